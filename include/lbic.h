@@ -1,0 +1,105 @@
+/* lbic.h -- C ABI of liblbic.so, the MI355X-native block-level masked-convolution codec.
+ *
+ * The reference's hot path is Python (graphs/models/BlockBasedImgCompLossy_net.py) over two native
+ * layers: torch conv/elementwise kernels and CompressAI's C++ coder.  Each entry point below replaces
+ * one reference interface (cited per function); the Python mirror in
+ * learned-block-based-image-compression_amd/lbic/ binds them with ctypes.
+ *
+ * Conventions
+ *   - All functions return 0 on success or a negative LBC_E* code; lbc_last_error() gives a
+ *     thread-local message.  LBC_E_NOT_UPDATED mirrors the reference's
+ *     ValueError("Uninitialized CDFs. Run update() first") (graphs/layers/entropy_layers_cai.py:185-204).
+ *   - Image tensors are block-major fp32: [n_img][Hb][Wb][C] with C = 3*B*B and channel index
+ *     (py*B + px)*3 + colour (arrange_block_pixels_to_channel_dim, agents/blkbsdimgcomp_agent.py:853-860).
+ *   - *_dev pointers are HIP device pointers owned by the caller; `stream` is a hipStream_t (NULL =
+ *     default stream).  The handle owns packed weights and workspaces; it is not thread-safe (the
+ *     reference is single-threaded, agents/blkbsdimgcomp_agent.py:565-566).
+ *   - Symbols / indexes are int32 in the reference's order: per image, raster block order, latent
+ *     channel minor (graphs/models/BlockBasedImgCompLossy_net.py:353-354).
+ */
+#ifndef LBIC_H
+#define LBIC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBC_OK 0
+#define LBC_E_ARG (-1)
+#define LBC_E_HIP (-2)
+#define LBC_E_STATE (-3)
+#define LBC_E_NOT_UPDATED (-4)
+#define LBC_E_STREAM (-5)
+
+typedef struct lbc_model lbc_model;
+
+typedef struct {
+    int block_size;  /* config.block_size (configs/<name>.json) */
+    int ks[4];       /* config.KS */
+    int n;           /* config.N */
+    int m;           /* config.M (latent channels) */
+    int device;      /* HIP device ordinal */
+} lbc_config;
+
+/* BlockBasedImgCompLossyNetv9.__init__ (net:259-317): allocate a model of this geometry. */
+int lbc_create(const lbc_config *cfg, lbc_model **out);
+void lbc_destroy(lbc_model *m);
+
+/* Module.load_state_dict for one tensor under its reference state-dict name
+ * (e.g. "prtr_forward3.0.gamma", "get_meanscale.6.bias").  Buffers (mask, pedestal, bound, the
+ * entropy-model buffers) are accepted and ignored: masks and reparametrisation constants are
+ * re-derived (masked_conv2d.py:9-17, utils/parametrizers.py:32-37). */
+int lbc_set_tensor(lbc_model *m, const char *ref_name, const float *host, const int64_t *shape, int ndim);
+
+/* Apply MaskedConv2d masks (masked_conv2d.py:19-21) and the GDN reparametrisation
+ * (gdn_compressai.py:66-68), pack every layer for the fp32 MFMA kernels and upload. */
+int lbc_finalize(lbc_model *m);
+
+/* compressai._CXX.pmf_to_quantized_cdf (called at entropy_layers_cai.py:61-64): host C++.
+ * cdf_out receives n+1 entries. */
+int lbc_pmf_to_quantized_cdf(const float *pmf, int n, int precision, uint32_t *cdf_out);
+
+/* GaussianConditional.update() results (entropy_layers_cai.py:590-613): the 64-entry scale table,
+ * quantized CDF rows [n_tables][cdf_stride], cdf lengths and offsets.  Until this is called,
+ * lbc_encode / lbc_decode return LBC_E_NOT_UPDATED. */
+int lbc_set_entropy_tables(lbc_model *m, const float *scale_table, int n_tables, const int32_t *cdf,
+                           int cdf_stride, const int32_t *cdf_length, const int32_t *offset);
+
+/* compress() closed loop (net:319-361) for a batch of images, on the GPU: x_dev [n_img][Hb][Wb][C]
+ * in [-1/2, 1/2] -> zhat_dev (same layout; the clamped reconstruction, net:357), sym_dev / idx_dev
+ * [n_img][Hb*Wb*M] int32, bits_dev (nullable) [n_img][Hb*Wb*M] fp32 = -log2 of the Gaussian likelihood
+ * (entropy_layers_cai.py:615-647, the per-latent self-information of net:103).  The raster
+ * dependency is scheduled as an anti-diagonal wavefront t = h + 2v over all images at once. */
+int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, float *zhat_dev,
+               int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, void *stream);
+
+/* BufferedRansEncoder.encode_with_indexes + flush (net:328,359-360), host C++, one image.
+ * *out is allocated by the library (release with lbc_free). */
+int lbc_rans_encode(const lbc_model *m, const int32_t *sym, const int32_t *idx, size_t n, uint8_t **out,
+                    size_t *len);
+
+/* RansDecoder host-side reference decode of a whole stream (net:409-410,439 for every block),
+ * given every symbol's table index: test/debug helper for the host coder. */
+int lbc_rans_decode_host(const lbc_model *m, const uint8_t *data, size_t len, const int32_t *idx, size_t n,
+                         int32_t *sym_out);
+
+/* decompress() (net:400-452) for a batch of images: streams[i] / lens[i] are the host bitstreams
+ * lbc_rans_encode produced.  Strictly raster-serial within an image (the reference format has one
+ * rANS stream per image); images are decoded together, rANS decode runs on the GPU. */
+int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
+               float *zhat_dev, void *stream);
+
+void lbc_free(void *p);
+const char *lbc_last_error(void);
+
+/* Kernel-time instrumentation of the last lbc_encode / lbc_decode call (HIP events on `stream`):
+ * total milliseconds of the encode and decode phases. */
+int lbc_last_timing(const lbc_model *m, double *enc_ms, double *dec_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBIC_H */

@@ -1,0 +1,682 @@
+// liblbic.so host side: model handle, state-dict loader and weight packing, wavefront / raster step
+// scheduler, and the C ABI declared in include/lbic.h.
+//
+// Encode (compress, net:319-361): the raster closed loop is replayed as a skewed anti-diagonal
+// wavefront.  Block (v, h) needs the reconstructions of (v-1, h-1..h+1), (v, h-1) (and, for KS[1] = 3,
+// of (v-2, h-2..h+2), (v-1, h-2), (v, h-2)), so every block with h + 2v = t depends only on steps < t
+// and all of them -- across every image of the batch -- are coded in one step of 18 GEMM launches.
+// Decode (decompress, net:400-452) keeps the reference's single raster-ordered rANS stream per image:
+// each raster step decodes the same block position of every image (ctx GEMMs -> GPU rANS -> decoder
+// GEMMs).  Both phases run the same k_gemm arithmetic, so decoder scale indexes equal the encoder's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "lbic_internal.h"
+
+namespace lbic {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return set_error(LBC_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int alloc(size_t b) {
+        if (b <= bytes && p) return LBC_OK;
+        release();
+        if (hipMalloc(&p, std::max<size_t>(b, 16)) != hipSuccess) {
+            p = nullptr;
+            return set_error(LBC_E_HIP, "hipMalloc failed");
+        }
+        bytes = b;
+        return LBC_OK;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Layer {
+    DevBuf W, bias;
+    int K = 0, N = 0, NB16 = 0;
+};
+
+struct HostT {
+    std::vector<float> v;
+    std::vector<int64_t> shape;
+};
+
+inline int pad16(int x) { return (x + 15) & ~15; }
+
+static const int TAPS_A[4][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}};       // masked_conv2d.py:9-17 'A'
+static const int TAPS_B[5][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0}};  // 'B' adds the centre
+
+}  // namespace lbic
+
+using namespace lbic;
+
+struct lbc_model {
+    lbc_config cfg{};
+    int B = 0, Cx = 0, N = 0, M = 0, N7 = 0, N6 = 0, C1 = 0, C2 = 0, C3 = 0, C4 = 0, P = 1;
+    int NP = 0, C1P = 0, C2P = 0, C3P = 0;   // widths padded to 16 (activation row strides)
+    std::map<std::string, HostT> host;
+    bool finalized = false;
+    Layer ctx0, ctx1, ctx2, ctx3, enc0, g0, e1, g1, e2, g2, e3, dec0, ig0, d1, ig1, d2, ig2, d3;
+    EntropyTables tabs;
+    bool tabs_set = false;
+    DevBuf table_dev, cdf16_dev, tmeta_dev;
+    int total16 = 0;
+    std::vector<uint16_t> c16_host;
+    std::vector<int> meta_host;
+    bool tabs_dirty = false;
+    // per-shape workspace
+    int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
+    DevBuf zpad, blocks_enc, blocks_dec, a_ctx0, a_ctx1, a_ctx2, a_ksi, a_e0, a_e1, a_yq, a_d0, a_d1, a_idx;
+    std::vector<int> step_off, step_cnt;
+    DevBuf words, word_base, word_count, st_x, st_ptr, st_status;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool enc_timed = false, dec_timed = false;
+};
+
+namespace {
+
+int dev_upload(DevBuf& d, const void* src, size_t bytes) {
+    int rc = d.alloc(bytes);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
+    return LBC_OK;
+}
+
+// Pack W[k][n] (row-major K x N, N padded to 16) into [K/16][N/16][4][16][4]: the float4 lane l of
+// a wave loads for a 16x16 k-n tile holds W[4*(l>>4) + e][l&15], e = 0..3 -- the A/B operand of four
+// v_mfma_f32_16x16x4_f32 (operand maps: cdna_hip_programming.md §3).
+int upload_layer(Layer& L, const std::vector<float>& wkn, const std::vector<float>& bias, int K, int N) {
+    if (K % 16) return set_error(LBC_E_ARG, "layer K not a multiple of 16");
+    const int NB = ((N + 31) / 32) * 2;   // whole 32-column tiles: the widest BN never reads past the end
+    std::vector<float> pk((size_t)K * NB * 16, 0.f);
+    for (int kb = 0; kb < K / 16; ++kb)
+        for (int nb = 0; nb < NB; ++nb)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 4; ++e) {
+                    const int k = kb * 16 + 4 * (l >> 4) + e, n = nb * 16 + (l & 15);
+                    pk[(((size_t)kb * NB + nb) * 64 + l) * 4 + e] = n < N ? wkn[(size_t)k * N + n] : 0.f;
+                }
+    std::vector<float> b(NB * 16, 0.f);
+    std::copy(bias.begin(), bias.end(), b.begin());
+    L.K = K;
+    L.N = N;
+    L.NB16 = NB;
+    int rc = dev_upload(L.W, pk.data(), pk.size() * 4);
+    if (rc) return rc;
+    return dev_upload(L.bias, b.data(), b.size() * 4);
+}
+
+const HostT* get(lbc_model* m, const std::string& n) {
+    auto it = m->host.find(n);
+    return it == m->host.end() ? nullptr : &it->second;
+}
+
+// conv weight [cout][cin][k][k] -> W[k = slot*cin + ci][n] for the listed taps (a 1x1 conv is one slot)
+// slot = K stride between taps (>= cin; padded columns keep zero weights)
+int conv_to_kn(lbc_model* m, const std::string& name, int cin, int cout, const int (*taps)[2], int ntaps,
+               std::vector<float>& wkn, int k_base, int slot, std::vector<float>* bias_acc) {
+    const HostT* w = get(m, name + ".weight");
+    const HostT* b = get(m, name + ".bias");
+    if (!w || !b) return set_error(LBC_E_STATE, "missing tensor " + name);
+    const int ks = (int)w->shape[2];
+    if ((int)w->shape[0] != cout || (int)w->shape[1] != cin || (int)b->v.size() != cout)
+        return set_error(LBC_E_ARG, "bad shape for " + name);
+    for (int t = 0; t < ntaps; ++t) {
+        const int ky = ks == 1 ? 0 : 1 + taps[t][0], kx = ks == 1 ? 0 : 1 + taps[t][1];
+        for (int ci = 0; ci < cin; ++ci)
+            for (int co = 0; co < cout; ++co)
+                wkn[(size_t)(k_base + t * slot + ci) * cout + co] = w->v[(((size_t)co * cin + ci) * ks + ky) * ks + kx];
+    }
+    if (bias_acc) {
+        if (bias_acc->empty()) bias_acc->assign(b->v.begin(), b->v.end());
+        else for (int co = 0; co < cout; ++co) (*bias_acc)[co] += b->v[co];
+    }
+    return LBC_OK;
+}
+
+int pack_conv(lbc_model* m, Layer& L, const std::string& name, int cin, int cout, int ntaps, const int (*taps)[2]) {
+    const int slot = pad16(cin);
+    std::vector<float> wkn((size_t)ntaps * slot * cout, 0.f), bias;
+    int rc = conv_to_kn(m, name, cin, cout, taps, ntaps, wkn, 0, slot, &bias);
+    if (rc) return rc;
+    return upload_layer(L, wkn, bias, ntaps * slot, cout);
+}
+
+// first layer of the encoder / decoder transform: 4 masked taps of prtr_*2 on zhat + the 1x1 prtr_*1
+// on x (or y_qnt), one GEMM (K = 4*Cx + cin1); bias = b1 + b2 (net:379-387: out_x + out_zhat).
+int pack_first(lbc_model* m, Layer& L, const std::string& n2, const std::string& n1, int cin1) {
+    const int K = 4 * m->Cx + cin1;
+    std::vector<float> wkn((size_t)K * m->N), bias;
+    int rc = conv_to_kn(m, n2, m->Cx, m->N, TAPS_A, 4, wkn, 0, m->Cx, &bias);
+    if (rc) return rc;
+    static const int one[1][2] = {{0, 0}};
+    rc = conv_to_kn(m, n1, cin1, m->N, one, 1, wkn, 4 * m->Cx, cin1, &bias);
+    if (rc) return rc;
+    return upload_layer(L, wkn, bias, K, m->N);
+}
+
+// GDN: norm_i = beta_i + sum_j gamma_ij x_j^2 with the reparametrisation of
+// utils/parametrizers.py:45-47: v -> max(v, bound)^2 - pedestal, pedestal = 2^-36,
+// bound = sqrt(minimum + pedestal) (beta_min = 1e-6, gdn_compressai.py:43-56).
+int pack_gdn(lbc_model* m, Layer& L, const std::string& name, int C) {
+    const HostT* be = get(m, name + ".beta");
+    const HostT* ga = get(m, name + ".gamma");
+    if (!be || !ga) return set_error(LBC_E_STATE, "missing tensor " + name);
+    if ((int)be->v.size() != C || (int)ga->v.size() != C * C) return set_error(LBC_E_ARG, "bad GDN shape " + name);
+    const float ped = (float)std::pow(2.0, -36.0);
+    const float bb = (float)std::sqrt(1e-6 + std::pow(2.0, -36.0));
+    const float gb = (float)std::sqrt(0.0 + std::pow(2.0, -36.0));
+    std::vector<float> beta(C), wkn((size_t)pad16(C) * C, 0.f);
+    for (int i = 0; i < C; ++i) {
+        const float t = std::max(be->v[i], bb);
+        beta[i] = t * t - ped;
+    }
+    for (int i = 0; i < C; ++i)
+        for (int j = 0; j < C; ++j) {
+            const float t = std::max(ga->v[(size_t)i * C + j], gb);
+            wkn[(size_t)j * C + i] = t * t - ped;       // W[k = j][n = i]
+        }
+    return upload_layer(L, wkn, beta, pad16(C), C);
+}
+
+int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
+    if (m->ws_n == n_img && m->ws_Hb == Hb && m->ws_Wb == Wb) return LBC_OK;
+    const int T = (Wb - 1) + 2 * (Hb - 1) + 1;
+    std::vector<int4> enc;
+    m->step_off.assign(T, 0);
+    m->step_cnt.assign(T, 0);
+    int mmax = n_img;
+    for (int t = 0; t < T; ++t) {
+        m->step_off[t] = (int)enc.size();
+        for (int img = 0; img < n_img; ++img)
+            for (int v = 0; v < Hb; ++v) {
+                const int h = t - 2 * v;
+                if (h >= 0 && h < Wb) enc.push_back(make_int4(img, v, h, 0));
+            }
+        m->step_cnt[t] = (int)enc.size() - m->step_off[t];
+        mmax = std::max(mmax, m->step_cnt[t]);
+    }
+    std::vector<int4> dec((size_t)Hb * Wb * n_img);
+    for (int s = 0; s < Hb * Wb; ++s)
+        for (int img = 0; img < n_img; ++img) dec[(size_t)s * n_img + img] = make_int4(img, s / Wb, s % Wb, 0);
+    int rc;
+    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4)))) return rc;
+    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4)))) return rc;
+    const size_t rows = (size_t)mmax;
+    const size_t F = sizeof(float);
+    if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
+    // activation widths are padded to 16 columns; the pad columns are zeroed once and never written,
+    // so GEMMs can run K over whole 16-wide k-blocks (their weights are zero there too)
+    DevBuf* bufs[] = {&m->a_ctx0, &m->a_ctx1, &m->a_ctx2, &m->a_ksi, &m->a_e0, &m->a_e1,
+                      &m->a_d0, &m->a_d1, &m->a_yq, &m->a_idx};
+    const size_t widths[] = {(size_t)m->P * m->C1P, (size_t)m->C2P, (size_t)m->C3P, (size_t)m->C4, (size_t)m->NP,
+                             (size_t)m->NP, (size_t)m->NP, (size_t)m->NP, (size_t)m->M, (size_t)m->M};
+    for (int i = 0; i < 10; ++i) {
+        if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
+        HIPCHK(hipMemset(bufs[i]->p, 0, rows * widths[i] * F));
+    }
+    m->Mmax = mmax;
+    m->ws_n = n_img;
+    m->ws_Hb = Hb;
+    m->ws_Wb = Wb;
+    return LBC_OK;
+}
+
+// first device use: events and the entropy tables (host copies made by lbc_set_entropy_tables)
+int prepare_device(lbc_model* m) {
+    HIPCHK(hipSetDevice(m->cfg.device));
+    if (!m->ev[0])
+        for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
+    if (m->tabs_dirty) {
+        int rc;
+        if ((rc = dev_upload(m->table_dev, m->tabs.table.data(), 64 * sizeof(float)))) return rc;
+        if ((rc = dev_upload(m->cdf16_dev, m->c16_host.data(), m->c16_host.size() * 2))) return rc;
+        if ((rc = dev_upload(m->tmeta_dev, m->meta_host.data(), m->meta_host.size() * sizeof(int)))) return rc;
+        m->tabs_dirty = false;
+    }
+    return LBC_OK;
+}
+
+GemmArgs base_args(lbc_model* m, const int4* blocks, int rows, const float* x, int n_img, int Hb, int Wb) {
+    GemmArgs g{};
+    g.M = rows;
+    g.P = 1;
+    g.blocks = blocks;
+    g.pos_dy[0] = g.pos_dx[0] = 0;
+    g.geo.zpad = m->zpad.as<float>();
+    g.geo.Hp = Hb + 2;
+    g.geo.Wp = Wb + 4;
+    g.geo.Cx = m->Cx;
+    g.geo.x = x;
+    g.geo.Hb = Hb;
+    g.geo.Wb = Wb;
+    g.table = m->table_dev.as<float>();
+    g.Mlat = m->M;
+    g.HW = Hb * Wb;
+    (void)n_img;
+    return g;
+}
+
+void set_layer(GemmArgs& g, const Layer& L, int epi, float* out, int ldo) {
+    g.W = L.W.as<float>();
+    g.bias = L.bias.as<float>();
+    g.NB16 = L.NB16;
+    g.K = L.K;
+    g.N = L.N;
+    g.epi = epi;
+    g.out = out;
+    g.ldo = ldo;
+}
+
+void seg_dense(GemmArgs& g, const float* base, int ld, int k0, int k1) {
+    Seg& s = g.seg[g.nseg++];
+    s = Seg{base, SEG_DENSE, ld, 0, 0, k0, k1};
+}
+
+void segs_ztaps(GemmArgs& g, int Cx) {
+    for (int t = 0; t < 4; ++t) {
+        Seg& s = g.seg[g.nseg++];
+        s = Seg{nullptr, SEG_ZTAP, 0, TAPS_A[t][0], TAPS_A[t][1], t * Cx, (t + 1) * Cx};
+    }
+}
+
+int run_dense(GemmArgs g, const Layer& L, const float* in, int ld_in, int epi, float* out, int ldo, hipStream_t s) {
+    g.nseg = 0;
+    g.square_a = 0;
+    set_layer(g, L, epi, out, ldo);
+    seg_dense(g, in, ld_in, 0, L.K);
+    return launch_gemm(g, s);
+}
+
+// ld: row stride of `in` and `out` (the padded activation width)
+int run_gdn(GemmArgs g, const Layer& L, const float* in, int ld, bool inverse, float* out, hipStream_t s) {
+    g.nseg = 0;
+    set_layer(g, L, inverse ? EPI_IGDN : EPI_GDN, out, ld);
+    seg_dense(g, in, ld, 0, L.K);
+    g.square_a = 1;
+    g.gx = in;
+    g.ldx = ld;
+    return launch_gemm(g, s);
+}
+
+// context net (get_meanscale_fast, net:389-398) for the rows of `g`; the last layer's epilogue is
+// plain (encode) or also emits the scale indexes (decode).
+int run_ctx(lbc_model* m, GemmArgs g, bool with_idx, hipStream_t s) {
+    int rc;
+    {
+        GemmArgs c = g;
+        c.nseg = 0;
+        c.square_a = 0;
+        c.P = m->P;
+        c.M = g.M * m->P;
+        for (int p = 0; p < m->P; ++p) {
+            c.pos_dy[p] = m->P == 1 ? 0 : TAPS_B[p][0];
+            c.pos_dx[p] = m->P == 1 ? 0 : TAPS_B[p][1];
+        }
+        set_layer(c, m->ctx0, EPI_LEAKY, m->a_ctx0.as<float>(), m->C1P);
+        segs_ztaps(c, m->Cx);
+        if ((rc = launch_gemm(c, s))) return rc;
+    }
+    if ((rc = run_dense(g, m->ctx1, m->a_ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, m->a_ctx1.as<float>(), m->C2P, s)))
+        return rc;
+    if ((rc = run_dense(g, m->ctx2, m->a_ctx1.as<float>(), m->C2P, EPI_LEAKY, m->a_ctx2.as<float>(), m->C3P, s)))
+        return rc;
+    GemmArgs c = g;
+    c.idx = m->a_idx.as<int32_t>();
+    return run_dense(c, m->ctx3, m->a_ctx2.as<float>(), m->C3P, with_idx ? EPI_CTXIDX : EPI_BIAS, m->a_ksi.as<float>(),
+                     m->C4, s);
+}
+
+// decoder transform (inverse_prtr_fast, net:384-387) + clamp + write-back into zpad (net:357)
+int run_dec(lbc_model* m, GemmArgs g, hipStream_t s) {
+    int rc;
+    {
+        GemmArgs c = g;
+        c.nseg = 0;
+        c.square_a = 0;
+        set_layer(c, m->dec0, EPI_BIAS, m->a_d0.as<float>(), m->NP);
+        segs_ztaps(c, m->Cx);
+        seg_dense(c, m->a_yq.as<float>(), m->M, 4 * m->Cx, 4 * m->Cx + m->M);
+        if ((rc = launch_gemm(c, s))) return rc;
+    }
+    float *d0 = m->a_d0.as<float>(), *d1 = m->a_d1.as<float>();
+    const int W = m->NP;
+    if ((rc = run_gdn(g, m->ig0, d0, W, true, d1, s))) return rc;
+    if ((rc = run_dense(g, m->d1, d1, W, EPI_BIAS, d0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->ig1, d0, W, true, d1, s))) return rc;
+    if ((rc = run_dense(g, m->d2, d1, W, EPI_BIAS, d0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->ig2, d0, W, true, d1, s))) return rc;
+    return run_dense(g, m->d3, d1, W, EPI_CLAMPZ, nullptr, 0, s);
+}
+
+// encoder transform (forward_prtr_fast, net:379-382) + quantize epilogue
+int run_enc(lbc_model* m, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, hipStream_t s) {
+    int rc;
+    float *e0 = m->a_e0.as<float>(), *e1 = m->a_e1.as<float>();
+    {
+        GemmArgs c = g;
+        c.nseg = 0;
+        c.square_a = 0;
+        set_layer(c, m->enc0, EPI_BIAS, e0, m->NP);
+        segs_ztaps(c, m->Cx);
+        Seg& sx = c.seg[c.nseg++];
+        sx = Seg{nullptr, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
+        if ((rc = launch_gemm(c, s))) return rc;
+    }
+    const int W = m->NP;
+    if ((rc = run_gdn(g, m->g0, e0, W, false, e1, s))) return rc;
+    if ((rc = run_dense(g, m->e1, e1, W, EPI_BIAS, e0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->g1, e0, W, false, e1, s))) return rc;
+    if ((rc = run_dense(g, m->e2, e1, W, EPI_BIAS, e0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->g2, e0, W, false, e1, s))) return rc;
+    GemmArgs c = g;
+    c.ksi = m->a_ksi.as<float>();
+    c.ldk = m->C4;
+    c.sym = sym;
+    c.idx = idx;
+    c.bits = bits;
+    return run_dense(c, m->e3, e1, W, EPI_QUANT, m->a_yq.as<float>(), m->M, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lbc_create(const lbc_config* cfg, lbc_model** out) {
+    if (!cfg || !out) return set_error(LBC_E_ARG, "null argument");
+    if (cfg->block_size <= 0 || cfg->n <= 0 || cfg->m <= 0 || cfg->ks[0] != 3 || (cfg->ks[1] != 1 && cfg->ks[1] != 3))
+        return set_error(LBC_E_ARG, "unsupported geometry (KS[0] must be 3, KS[1] 1 or 3)");
+    if (cfg->ks[2] != 1 && cfg->ks[2] != 3) return set_error(LBC_E_ARG, "bad KS");
+    auto* m = new lbc_model();   // no HIP call here: host-only entry points work without a GPU
+    m->cfg = *cfg;
+    m->B = cfg->block_size;
+    m->Cx = 3 * m->B * m->B;
+    m->N = cfg->n;
+    m->M = cfg->m;
+    m->N7 = m->N / 8 * 7;
+    m->N6 = m->N / 8 * 6;
+    m->C1 = m->N / 8 * 12;
+    m->C2 = m->N / 8 * 10;
+    m->C3 = m->N / 8 * 8;
+    m->C4 = 2 * m->M;
+    m->NP = pad16(m->N);
+    m->C1P = pad16(m->C1);
+    m->C2P = pad16(m->C2);
+    m->C3P = pad16(m->C3);
+    if (m->Cx % 16 || m->M % 16) {
+        delete m;
+        return set_error(LBC_E_ARG, "3*B^2 and M must be multiples of 16");
+    }
+    m->P = cfg->ks[1] == 3 ? 5 : 1;
+    *out = m;
+    return LBC_OK;
+}
+
+void lbc_destroy(lbc_model* m) {
+    if (!m) return;
+    for (auto& e : m->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete m;
+}
+
+int lbc_set_tensor(lbc_model* m, const char* name, const float* host, const int64_t* shape, int ndim) {
+    if (!m || !name || !host || (ndim > 0 && !shape)) return set_error(LBC_E_ARG, "null argument");
+    std::string n(name);
+    auto ends = [&](const char* suf) {
+        const size_t l = strlen(suf);
+        return n.size() >= l && n.compare(n.size() - l, l, suf) == 0;
+    };
+    if (ends(".mask") || ends(".pedestal") || ends(".bound") || n.rfind("conditional_gaussian_model.", 0) == 0)
+        return LBC_OK;   // derived constants / entropy buffers (set through lbc_set_entropy_tables)
+    HostT t;
+    size_t cnt = 1;
+    for (int i = 0; i < ndim; ++i) {
+        t.shape.push_back(shape[i]);
+        cnt *= (size_t)shape[i];
+    }
+    t.v.assign(host, host + cnt);
+    m->host[n] = std::move(t);
+    m->finalized = false;
+    return LBC_OK;
+}
+
+int lbc_finalize(lbc_model* m) {
+    if (!m) return set_error(LBC_E_ARG, "null model");
+    HIPCHK(hipSetDevice(m->cfg.device));
+    const int Cx = m->Cx, N = m->N, M = m->M;
+    static const int one[1][2] = {{0, 0}};
+    int rc;
+    // context net: layer 0 = 4 masked taps; layer 1 = 1x1, or 3x3 'B' over the 5 layer-0 positions
+    if ((rc = pack_conv(m, m->ctx0, "get_meanscale.0", Cx, m->C1, 4, TAPS_A))) return rc;
+    if (m->P == 5) rc = pack_conv(m, m->ctx1, "get_meanscale.2", m->C1, m->C2, 5, TAPS_B);
+    else rc = pack_conv(m, m->ctx1, "get_meanscale.2", m->C1, m->C2, 1, one);
+    if (rc) return rc;
+    if ((rc = pack_conv(m, m->ctx2, "get_meanscale.4", m->C2, m->C3, 1, one))) return rc;
+    if ((rc = pack_conv(m, m->ctx3, "get_meanscale.6", m->C3, m->C4, 1, one))) return rc;
+    if ((rc = pack_first(m, m->enc0, "prtr_forward2", "prtr_forward1", Cx))) return rc;
+    if ((rc = pack_gdn(m, m->g0, "prtr_forward3.0", N))) return rc;
+    if ((rc = pack_conv(m, m->e1, "prtr_forward3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->g1, "prtr_forward3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, m->e2, "prtr_forward3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->g2, "prtr_forward3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, m->e3, "prtr_forward3.5", m->N6, M, 1, one))) return rc;
+    if ((rc = pack_first(m, m->dec0, "prtr_inverse2", "prtr_inverse1", M))) return rc;
+    if ((rc = pack_gdn(m, m->ig0, "prtr_inverse3.0", N))) return rc;
+    if ((rc = pack_conv(m, m->d1, "prtr_inverse3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->ig1, "prtr_inverse3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, m->d2, "prtr_inverse3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->ig2, "prtr_inverse3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, m->d3, "prtr_inverse3.5", m->N6, Cx, 1, one))) return rc;
+    m->finalized = true;
+    return LBC_OK;
+}
+
+int lbc_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf_out) {
+    if (!pmf || !cdf_out) return set_error(LBC_E_ARG, "null argument");
+    return pmf_to_quantized_cdf(pmf, n, precision, cdf_out);
+}
+
+int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables, const int32_t* cdf, int cdf_stride,
+                           const int32_t* cdf_length, const int32_t* offset) {
+    if (!m || !scale_table || !cdf || !cdf_length || !offset) return set_error(LBC_E_ARG, "null argument");
+    if (n_tables != 64) return set_error(LBC_E_ARG, "expected the 64-entry scale table (net:13-18)");
+    EntropyTables& t = m->tabs;
+    t.n_tables = n_tables;
+    t.stride = cdf_stride;
+    t.table.assign(scale_table, scale_table + n_tables);
+    t.cdf.assign(cdf, cdf + (size_t)n_tables * cdf_stride);
+    t.length.assign(cdf_length, cdf_length + n_tables);
+    t.offset.assign(offset, offset + n_tables);
+    // device copies: scale table, and 16-bit CDF rows for the GPU rANS decoder
+    std::vector<uint16_t> c16;
+    std::vector<int> meta(3 * 64, 0);
+    for (int i = 0; i < n_tables; ++i) {
+        const int len = t.length[i];
+        if (len < 3 || len > cdf_stride) return set_error(LBC_E_ARG, "bad cdf length");
+        meta[i] = (int)c16.size();
+        meta[64 + i] = len;
+        meta[128 + i] = t.offset[i];
+        for (int j = 0; j < len - 1; ++j) {
+            const int32_t v = cdf[(size_t)i * cdf_stride + j];
+            if (v < 0 || v > 65535) return set_error(LBC_E_ARG, "cdf entry out of 16-bit range");
+            c16.push_back((uint16_t)v);
+        }
+        c16.push_back(0);   // slot of the implicit final 2^16
+    }
+    if (c16.size() & 1) c16.push_back(0);
+    if (c16.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
+    m->total16 = (int)c16.size();
+    m->c16_host = std::move(c16);
+    m->meta_host = std::move(meta);
+    m->tabs_set = true;
+    m->tabs_dirty = true;
+    return LBC_OK;
+}
+
+int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, float* zhat_dev, int32_t* sym_dev,
+               int32_t* idx_dev, float* bits_dev, void* stream) {
+    if (!m || !x_dev || !zhat_dev || !sym_dev || !idx_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    HIPCHK(hipEventRecord(m->ev[0], s));
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    const int4* blocks = m->blocks_enc.as<int4>();
+    for (size_t t = 0; t < m->step_off.size(); ++t) {
+        const int rows = m->step_cnt[t];
+        GemmArgs g = base_args(m, blocks + m->step_off[t], rows, x_dev, n_img, Hb, Wb);
+        if ((rc = run_ctx(m, g, false, s))) return rc;
+        if ((rc = run_enc(m, g, sym_dev, idx_dev, bits_dev, s))) return rc;
+        if ((rc = run_dec(m, g, s))) return rc;
+    }
+    if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
+    HIPCHK(hipEventRecord(m->ev[1], s));
+    m->enc_timed = true;
+    return LBC_OK;
+}
+
+int lbc_rans_encode(const lbc_model* m, const int32_t* sym, const int32_t* idx, size_t n, uint8_t** out, size_t* len) {
+    if (!m || !sym || !idx || !out || !len) return set_error(LBC_E_ARG, "null argument");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    std::vector<uint8_t> bytes;
+    int rc = rans_encode(m->tabs, sym, idx, n, bytes);
+    if (rc) return rc;
+    *out = static_cast<uint8_t*>(malloc(std::max<size_t>(bytes.size(), 1)));
+    std::memcpy(*out, bytes.data(), bytes.size());
+    *len = bytes.size();
+    return LBC_OK;
+}
+
+int lbc_rans_decode_host(const lbc_model* m, const uint8_t* data, size_t len, const int32_t* idx, size_t n,
+                         int32_t* sym_out) {
+    if (!m || !data || !idx || !sym_out) return set_error(LBC_E_ARG, "null argument");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    return rans_decode_host(m->tabs, data, len, idx, n, sym_out);
+}
+
+int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, int n_img, int Hb, int Wb,
+               float* zhat_dev, void* stream) {
+    if (!m || !streams || !lens || !zhat_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    // streams -> device; initial rANS state = the first two words (Rans64DecInit)
+    std::vector<long long> base(n_img);
+    std::vector<int> cnt(n_img), ptr(n_img, 2);
+    std::vector<unsigned long long> x0(n_img);
+    size_t total = 0;
+    for (int i = 0; i < n_img; ++i) {
+        if (!streams[i] || lens[i] < 8 || (lens[i] & 3)) return set_error(LBC_E_STREAM, "invalid bitstream");
+        base[i] = (long long)(total / 4);
+        cnt[i] = (int)(lens[i] / 4);
+        total += lens[i];
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(streams[i]);
+        x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
+    }
+    std::vector<uint8_t> cat(total);
+    for (int i = 0, off = 0; i < n_img; off += (int)lens[i], ++i) std::memcpy(cat.data() + off, streams[i], lens[i]);
+    if ((rc = dev_upload(m->words, cat.data(), cat.size()))) return rc;
+    if ((rc = dev_upload(m->word_base, base.data(), base.size() * sizeof(long long)))) return rc;
+    if ((rc = dev_upload(m->word_count, cnt.data(), cnt.size() * sizeof(int)))) return rc;
+    if ((rc = dev_upload(m->st_x, x0.data(), x0.size() * sizeof(unsigned long long)))) return rc;
+    if ((rc = dev_upload(m->st_ptr, ptr.data(), ptr.size() * sizeof(int)))) return rc;
+    if ((rc = m->st_status.alloc(n_img * sizeof(int)))) return rc;
+    HIPCHK(hipMemsetAsync(m->st_status.p, 0, n_img * sizeof(int), s));
+    HIPCHK(hipEventRecord(m->ev[2], s));
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    RansArgs ra{};
+    ra.cdf16 = m->cdf16_dev.as<uint16_t>();
+    ra.tmeta = m->tmeta_dev.as<int>();
+    ra.total16 = m->total16;
+    ra.words = m->words.as<uint32_t>();
+    ra.word_base = m->word_base.as<long long>();
+    ra.word_count = m->word_count.as<int>();
+    ra.state_x = m->st_x.as<unsigned long long>();
+    ra.state_ptr = m->st_ptr.as<int>();
+    ra.status = m->st_status.as<int>();
+    ra.idx = m->a_idx.as<int32_t>();
+    ra.ksi = m->a_ksi.as<float>();
+    ra.ldk = m->C4;
+    ra.Mlat = m->M;
+    ra.yq = m->a_yq.as<float>();
+    ra.ldy = m->M;
+    ra.rows = n_img;
+    for (int st = 0; st < Hb * Wb; ++st) {
+        const int4* blocks = m->blocks_dec.as<int4>() + (size_t)st * n_img;
+        GemmArgs g = base_args(m, blocks, n_img, nullptr, n_img, Hb, Wb);
+        if ((rc = run_ctx(m, g, true, s))) return rc;
+        ra.blocks = blocks;
+        if ((rc = launch_rans_decode(ra, s))) return rc;
+        if ((rc = run_dec(m, g, s))) return rc;
+    }
+    if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
+    HIPCHK(hipEventRecord(m->ev[3], s));
+    m->dec_timed = true;
+    std::vector<int> status(n_img);
+    HIPCHK(hipMemcpyAsync(status.data(), m->st_status.p, n_img * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < n_img; ++i)
+        if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream for image " + std::to_string(i));
+    return LBC_OK;
+}
+
+void lbc_free(void* p) { free(p); }
+
+const char* lbc_last_error(void) { return g_err.c_str(); }
+
+int lbc_last_timing(const lbc_model* m, double* enc_ms, double* dec_ms) {
+    if (!m) return set_error(LBC_E_ARG, "null model");
+    float t = 0.f;
+    if (enc_ms) {
+        *enc_ms = -1.0;
+        if (m->enc_timed && hipEventSynchronize(m->ev[1]) == hipSuccess &&
+            hipEventElapsedTime(&t, m->ev[0], m->ev[1]) == hipSuccess)
+            *enc_ms = t;
+    }
+    if (dec_ms) {
+        *dec_ms = -1.0;
+        if (m->dec_timed && hipEventSynchronize(m->ev[3]) == hipSuccess &&
+            hipEventElapsedTime(&t, m->ev[2], m->ev[3]) == hipSuccess)
+            *dec_ms = t;
+    }
+    return LBC_OK;
+}
+
+}  // extern "C"

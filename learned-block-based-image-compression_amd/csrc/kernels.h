@@ -1,0 +1,86 @@
+// Kernel argument blocks and launchers (kernels.hip).  Device-side data layout:
+//   x     [n_img][Hb][Wb][Cx]            fp32, block-major (Cx = 3 B^2)
+//   zpad  [n_img][Hb+2][Wb+4][Cx]        fp32 reconstruction with a zero border: block (v,h) at
+//                                        [v+2][h+2]; rows -2,-1 and columns -2,-1,Wb,Wb+1 stay zero, so
+//                                        every window gather of the reference (zero pad outside the
+//                                        frame, net:342-351) is a plain load.
+//   W     [K/16][N/16][4][16][4]         packed fp32 weights of one GEMM (see pack_weights in codec.hip)
+//   acts  [rows][width]                  per-step activations, row = block (or block x position)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lbic {
+
+constexpr int KSPLIT = 8;   // every GEMM output = ((s0 + s1) + ... + s7) + bias, s_i = k-ordered fma chain
+                            // over the i-th eighth of K: identical for every tile shape, so the encoder
+                            // (large wavefront M) and the decoder (M = n_img) compute bit-identical values.
+
+enum SegKind : int { SEG_DENSE = 0, SEG_ZTAP = 1, SEG_X = 2 };
+enum Epi : int { EPI_BIAS = 0, EPI_LEAKY, EPI_GDN, EPI_IGDN, EPI_QUANT, EPI_CTXIDX, EPI_CLAMPZ };
+
+struct Seg {                 // one K-range of the A operand: K columns [k0, k1)
+    const float* base;       // SEG_DENSE: activations base
+    int kind;
+    int ld;                  // SEG_DENSE row stride (floats)
+    int dy, dx;              // SEG_ZTAP: tap offset relative to the output position
+    int k0, k1;
+};
+
+struct Geo {
+    float* zpad;
+    int Hp, Wp, Cx;
+    const float* x;
+    int Hb, Wb;
+};
+
+struct GemmArgs {
+    int M, N, K, P;          // P: A rows per block (context layer 0 positions); rows = blocks * P
+    int nseg;
+    Seg seg[6];
+    int pos_dy[5], pos_dx[5];
+    const int4* blocks;      // per block (img, v, h, 0); row r belongs to block r / P
+    const float* W;
+    int NB16;                // N padded / 16
+    const float* bias;       // bias (beta for GDN)
+    int epi, square_a;
+    float* out;
+    int ldo;
+    const float* gx;         // GDN: the layer input x (epilogue x * rsqrt(norm))
+    int ldx;
+    const float* ksi;        // EPI_QUANT: context output [rows][2*Mlat] (scales | means)
+    int ldk, Mlat;
+    const float* table;      // scale table (64)
+    int32_t* sym;            // EPI_QUANT: [n_img][HW*Mlat]; EPI_CTXIDX: idx_ws [rows][Mlat] in `idx`
+    int32_t* idx;
+    float* bits;
+    int HW;
+    Geo geo;
+};
+
+struct RansArgs {
+    const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit)
+    const int* tmeta;        // [3][64]: base, cdf_length, offset
+    int total16;             // entries in cdf16 (even)
+    const uint32_t* words;   // concatenated streams
+    const long long* word_base;
+    const int* word_count;
+    unsigned long long* state_x;
+    int* state_ptr;
+    int* status;             // non-zero: stream overrun / bad index (per image)
+    const int32_t* idx;      // [rows][Mlat]
+    const float* ksi;
+    int ldk, Mlat;
+    float* yq;
+    int ldy;
+    const int4* blocks;
+    int rows;
+};
+
+int launch_gemm(const GemmArgs& g, hipStream_t s);
+int launch_rans_decode(const RansArgs& a, hipStream_t s);
+int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
+
+}  // namespace lbic

@@ -1,0 +1,202 @@
+"""``BlockBasedImgCompLossyNetv9`` -- the reference's model interface over liblbic.so.
+
+Mirrors graphs/models/BlockBasedImgCompLossy_net.py:251-452: the same constructor argument (the
+config), ``load_state_dict`` with the reference's keys, ``update(force)``, ``compress(x, LRU, chlat)``
+-> (bitstream, zhat) and ``decompress(bitstream, LRU, xshape, chlat, devc)`` -> zhat, on the same NCHW
+block->channel tensors [1, 3B^2, H/B, W/B].  The arithmetic runs in HIP kernels; there is no CPU path.
+``compress_batch`` / ``decompress_batch`` add the batched form used by bench.py (BASELINE config 2:
+a batch of 32 frames on one GPU) on block-major [n, Hb, Wb, 3B^2] device tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arch import Arch, arch_from_config
+from .entropy import GaussianConditional, get_scale_table
+
+
+class BlockBasedImgCompLossyNetv9:
+    def __init__(self, config, device=None):
+        self.config = config
+        self.arch: Arch = arch_from_config(config)
+        if self.arch.KS[0] != 3:
+            raise ValueError("KS[0] must be 3 (all reference configs)")
+        if device is None:
+            device = torch.device("cuda", int(getattr(config, "gpu_device", 0) or 0))
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("BlockBasedImgCompLossyNetv9 runs on the GPU only (HIP kernels, no CPU path)")
+        self.conditional_gaussian_model = GaussianConditional()
+        self._params: Dict[str, torch.Tensor] = {}
+        cfg = _lib.LbcConfig()
+        cfg.block_size = self.arch.B
+        for i, k in enumerate(self.arch.KS):
+            cfg.ks[i] = k
+        cfg.n, cfg.m = self.arch.N, self.arch.M
+        cfg.device = self.device.index or 0
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().lbc_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self._tables_uploaded = False
+        self.training = False
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().lbc_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------------ nn.Module-like surface
+    def eval(self):
+        self.training = False
+        return self
+
+    def to(self, device):
+        if torch.device(device) != self.device:
+            raise RuntimeError("device is fixed at construction (one handle per GPU)")
+        return self
+
+    def parameters(self):
+        return iter(self._params.values())
+
+    def state_dict(self):
+        sd = dict(self._params)
+        sd.update(self.conditional_gaussian_model.state_dict())
+        return sd
+
+    def load_state_dict(self, sd, strict: bool = True):
+        """Reference keys (arch.param_shapes); buffers (mask, pedestal, bound) are accepted."""
+        names = {n for n, _ in self.arch.param_shapes()}
+        missing = [n for n in names if n not in sd]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}...")
+        L = _lib.lib()
+        for k, v in sd.items():
+            if k.startswith("conditional_gaussian_model."):
+                continue
+            t = torch.as_tensor(np.asarray(v) if not torch.is_tensor(v) else v).detach().float().cpu().contiguous()
+            if k in names:
+                self._params[k] = t
+            shape = (ctypes.c_int64 * t.dim())(*t.shape)
+            _lib.check(L.lbc_set_tensor(self._h, k.encode(), _lib.ptr(t), shape, t.dim()))
+        _lib.check(L.lbc_finalize(self._h))
+        return self
+
+    # ------------------------------------------------------------------ entropy model
+    def update(self, force=False):
+        """net:121-125: build the scale table and the quantized CDFs; pushes them to the device."""
+        updated = self.conditional_gaussian_model.update_scale_table(get_scale_table(), force=force)
+        if updated or not self._tables_uploaded:
+            self._upload_tables()
+        return updated
+
+    def _upload_tables(self):
+        gc = self.conditional_gaussian_model
+        gc._check_cdf_size()
+        gc._check_cdf_length()
+        gc._check_offsets_size()
+        table = gc.scale_table.float().contiguous().numpy()
+        cdf = gc.quantized_cdf.int().contiguous().numpy()
+        ln = gc.cdf_length.int().contiguous().numpy()
+        off = gc.offset.int().contiguous().numpy()
+        _lib.check(_lib.lib().lbc_set_entropy_tables(self._h, _lib.ptr(table), len(table), _lib.ptr(cdf),
+                                                     cdf.shape[1], _lib.ptr(ln), _lib.ptr(off)))
+        self._keep = (table, cdf, ln, off)
+        self._tables_uploaded = True
+
+    def _check_ready(self):
+        gc = self.conditional_gaussian_model
+        gc._check_cdf_size()
+        gc._check_cdf_length()
+        gc._check_offsets_size()
+        if not self._tables_uploaded:
+            self._upload_tables()
+
+    def _check_lru(self, LRU):
+        if LRU is not None and tuple(int(v) for v in LRU) != (self.arch.lru,) * 3:
+            raise ValueError(f"LRU {list(LRU)} != compress/decompress receptive field {[self.arch.lru] * 3} "
+                             "(agents/blkbsdimgcomp_agent.py:481-489)")
+
+    # ------------------------------------------------------------------ batched GPU path
+    def compress_batch(self, xb: torch.Tensor, want_bits: bool = False):
+        """xb: [n, Hb, Wb, 3B^2] fp32 on this device.  Returns dict(streams, zhat, symbols, indexes, bits)
+        with device tensors (symbols/indexes [n, Hb*Wb*M] int32, zhat like xb)."""
+        self._check_ready()
+        if xb.device != self.device or xb.dtype != torch.float32 or xb.dim() != 4 or xb.shape[3] != self.arch.cx:
+            raise ValueError("xb must be [n, Hb, Wb, 3B^2] float32 on the model's device")
+        xb = xb.contiguous()
+        n, Hb, Wb, _ = xb.shape
+        zhat = torch.empty_like(xb)
+        nsym = Hb * Wb * self.arch.M
+        sym = torch.empty((n, nsym), dtype=torch.int32, device=self.device)
+        idx = torch.empty((n, nsym), dtype=torch.int32, device=self.device)
+        bits = torch.empty((n, nsym), dtype=torch.float32, device=self.device) if want_bits else None
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(_lib.lib().lbc_encode(self._h, _lib.ptr(xb), n, Hb, Wb, _lib.ptr(zhat), _lib.ptr(sym),
+                                         _lib.ptr(idx), _lib.ptr(bits) if bits is not None else None,
+                                         ctypes.c_void_p(stream)))
+        return dict(zhat=zhat, symbols=sym, indexes=idx, bits=bits)
+
+    def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor) -> List[bytes]:
+        """BufferedRansEncoder per image (host C++), symbols/indexes [n, L] (any device)."""
+        s = symbols.to("cpu", torch.int32).contiguous().numpy()
+        i = indexes.to("cpu", torch.int32).contiguous().numpy()
+        out = []
+        L = _lib.lib()
+        for k in range(s.shape[0]):
+            p = ctypes.c_void_p()
+            ln = ctypes.c_size_t()
+            _lib.check(L.lbc_rans_encode(self._h, _lib.ptr(s[k]), _lib.ptr(i[k]), s.shape[1], ctypes.byref(p),
+                                         ctypes.byref(ln)))
+            out.append(ctypes.string_at(p, ln.value))
+            L.lbc_free(p)
+        return out
+
+    def decompress_batch(self, streams: Sequence[bytes], Hb: int, Wb: int) -> torch.Tensor:
+        """Decode n bitstreams of Hb x Wb blocks on the GPU -> zhat [n, Hb, Wb, 3B^2]."""
+        self._check_ready()
+        n = len(streams)
+        bufs = [ctypes.create_string_buffer(bytes(s), len(s)) for s in streams]
+        arr = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        lens = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+        zhat = torch.empty((n, Hb, Wb, self.arch.cx), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(_lib.lib().lbc_decode(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
+        return zhat
+
+    def last_timing(self):
+        e, d = ctypes.c_double(), ctypes.c_double()
+        _lib.check(_lib.lib().lbc_last_timing(self._h, ctypes.byref(e), ctypes.byref(d)))
+        return e.value, d.value
+
+    # ------------------------------------------------------------------ reference interface
+    def compress(self, x, LRU, chlat):
+        """net:319-361.  x: [1, 3B^2, H/B, W/B] in [-1/2, 1/2] -> (bitstream, zhat [1, 3B^2, H/B, W/B])."""
+        self._check_lru(LRU)
+        if chlat != self.arch.M:
+            raise ValueError("chlat must equal config.M")
+        if x.dim() != 4 or x.shape[0] != 1:
+            raise ValueError("compress() takes one image [1, 3B^2, H/B, W/B] (the reference is batch-1)")
+        xb = x.to(self.device, torch.float32).permute(0, 2, 3, 1).contiguous()
+        r = self.compress_batch(xb)
+        stream = self.entropy_encode(r["symbols"], r["indexes"])[0]
+        return stream, r["zhat"].permute(0, 3, 1, 2).contiguous()
+
+    def decompress(self, bitstream, LRU, xshape, chlat, devc=None):
+        """net:400-452 -> zhat [1, 3B^2, H/B, W/B] on this model's device."""
+        self._check_lru(LRU)
+        if chlat != self.arch.M:
+            raise ValueError("chlat must equal config.M")
+        bt, ch, hg, wd = (int(v) for v in xshape)
+        if bt != 1 or ch != self.arch.cx:
+            raise ValueError("xshape must be [1, 3B^2, H/B, W/B]")
+        z = self.decompress_batch([bitstream], hg, wd)
+        return z.permute(0, 3, 1, 2).contiguous()

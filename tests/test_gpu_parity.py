@@ -1,0 +1,156 @@
+"""GPU parity: the HIP path (liblbic.so through the C ABI) against the reference golden vectors and the
+oracle.  Bars: symbols and scale indexes bit-exact (tie-screened fixtures), reconstructions within
+1e-5 absolute on [-1/2, 1/2] pixels, bitstream bytes identical to the oracle coder on the same
+symbols, decode(encode) bit-exact, estimated bits within 1e-4 relative of the oracle likelihood."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_arch, load_golden
+from lbic.weights import synth_state_dict
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows"]
+_MODELS = {}
+
+
+def model_for(arch, seed=1337):
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    key = (arch, seed)
+    if key not in _MODELS:
+        cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
+        m = BlockBasedImgCompLossyNetv9(cfg)
+        m.load_state_dict(synth_state_dict(arch, seed))
+        m.update(force=True)
+        _MODELS[key] = m
+    return _MODELS[key]
+
+
+@pytest.fixture(scope="module")
+def tables():
+    return O.GaussianTables()
+
+
+@pytest.mark.parametrize("name", LOOPS)
+def test_closed_loop_matches_reference(name, tables):
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    x = torch.from_numpy(g["x"])[None].cuda()
+    r = m.compress_batch(x, want_bits=True)
+    sym = r["symbols"][0].cpu().numpy()
+    idx = r["indexes"][0].cpu().numpy()
+    assert np.array_equal(idx, g["indexes"]), f"{(idx != g['indexes']).sum()} index mismatches"
+    assert np.array_equal(sym, g["symbols"]), f"{(sym != g['symbols']).sum()} symbol mismatches"
+    z = r["zhat"][0].cpu().numpy()
+    assert np.abs(z - g["zhat"]).max() < 1e-5
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    assert streams[0] == tables.encode(g["symbols"], g["indexes"])
+    zdec = m.decompress_batch(streams, *g["x"].shape[:2])
+    assert torch.equal(zdec, r["zhat"]), "decoder reconstruction differs from the encoder's"
+
+
+def test_bits_match_oracle_likelihood():
+    g = load_golden("stages_b8_lowrate")
+    loop = load_golden("loop_b8_lowrate_2rows")
+    arch = golden_arch(loop)
+    m = model_for(arch)
+    r = m.compress_batch(torch.from_numpy(loop["x"])[None].cuda(), want_bits=True)
+    bits = r["bits"][0].cpu().numpy().reshape(loop["x"].shape[0], loop["x"].shape[1], arch.M)
+    for bi, (v, h) in enumerate(g["blocks"]):
+        ref = g["bits"][bi]
+        assert np.abs(bits[v, h] - ref).max() <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_batch_equals_single():
+    """Images coded together (one wavefront over the batch) give bit-identical results to one at a time."""
+    g = load_golden("loop_tiny_ks3311")
+    arch = golden_arch(g)
+    m = model_for(arch)
+    rng = np.random.default_rng(5)
+    imgs = [O.image_to_blocks(rng.integers(0, 256, (3, 32, 48)).astype(np.float32) / 255 - 0.5, 4) for _ in range(3)]
+    xb = torch.from_numpy(np.stack(imgs)).cuda()
+    rb = m.compress_batch(xb)
+    for k in range(3):
+        r1 = m.compress_batch(xb[k:k + 1].contiguous())
+        assert torch.equal(r1["symbols"][0], rb["symbols"][k])
+        assert torch.equal(r1["zhat"][0], rb["zhat"][k])
+    streams = m.entropy_encode(rb["symbols"], rb["indexes"])
+    assert torch.equal(m.decompress_batch(streams, 8, 12), rb["zhat"])
+
+
+def test_reference_interface_roundtrip():
+    """compress(x, LRU, chlat) / decompress(...) on the reference's NCHW block->channel tensors."""
+    g = load_golden("loop_tiny_ks3111")
+    arch = golden_arch(g)
+    m = model_for(arch)
+    x = torch.from_numpy(g["x"]).permute(2, 0, 1)[None].cuda()         # [1, 3B^2, Hb, Wb]
+    lru = [arch.lru] * 3
+    bs, zhat = m.compress(x, lru, arch.M)
+    assert isinstance(bs, bytes) and len(bs) % 4 == 0
+    zdec = m.decompress(bs, lru, x.shape, arch.M, x.device)
+    assert torch.equal(zhat, zdec)
+    assert np.abs(zhat[0].permute(1, 2, 0).cpu().numpy() - g["zhat"]).max() < 1e-5
+    with pytest.raises(ValueError):
+        m.compress(x, [arch.lru + 1] * 3, arch.M)
+
+
+def test_uninitialized_cdf_raises():
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    from lbic.arch import Arch
+    arch = Arch(4, (3, 1, 1, 1), 64, 16)
+    cfg = types.SimpleNamespace(block_size=4, KS=[3, 1, 1, 1], N=64, M=16, gpu_device=0)
+    m = BlockBasedImgCompLossyNetv9(cfg)
+    m.load_state_dict(synth_state_dict(arch, 1))
+    with pytest.raises(ValueError, match="Run update"):
+        m.compress_batch(torch.zeros(1, 2, 2, 48, device="cuda"))
+
+
+def _teacher_forced_check(arch, xb, zhat, sym, idx, blocks):
+    """Recompute sampled blocks on the CPU oracle given the GPU's own reconstruction (teacher forcing):
+    symbols/indexes must agree wherever the oracle's rounding / table margins exceed 1e-4."""
+    net = O.OracleNet(arch, synth_state_dict(arch, 1337))
+    table = O.scale_table()
+    L, M = arch.lru, arch.M
+    Hb, Wb, C = xb.shape
+    zp = np.zeros((Hb + 2 * L, Wb + 2 * L, C), np.float32)
+    zp[L:L + Hb, L:L + Wb] = zhat
+    checked = 0
+    for (v, h) in blocks:
+        win = zp[v:v + 2 * L + 1, h:h + 2 * L + 1].copy()
+        win[L, L:] = 0
+        win[L + 1:] = 0
+        ksi = net.ctx(win)
+        y = net.fwd(win, xb[v, h])
+        d = (y - ksi[M:]).astype(np.float64)
+        ok = np.abs(np.abs(d - np.floor(d)) - 0.5) > 1e-4
+        s_ref = np.rint(d).astype(np.int32)
+        sl = slice((v * Wb + h) * M, (v * Wb + h + 1) * M)
+        assert np.array_equal(sym[sl][ok], s_ref[ok])
+        raw = ksi[:M].astype(np.float64)
+        okx = np.min(np.abs(raw[:, None] - table[None, :]) / table[None, :], axis=1) > 1e-4
+        assert np.array_equal(idx[sl][okx], O.build_indexes(ksi[:M], table)[okx])
+        checked += 1
+    return checked
+
+
+def test_large_frame_b8_lowrate_roundtrip_and_teacher_forced():
+    """B8_lowrate at 2 x 256x256: decode(encode) bit-exact; sampled blocks agree with the oracle."""
+    from lbic.arch import Arch
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    m = model_for(arch)
+    rng = np.random.default_rng(11)
+    imgs = np.stack([O.image_to_blocks(rng.integers(0, 256, (3, 256, 256)).astype(np.float32) / 255 - 0.5, 8)
+                     for _ in range(2)])
+    xb = torch.from_numpy(imgs).cuda()
+    r = m.compress_batch(xb)
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    assert torch.equal(m.decompress_batch(streams, 32, 32), r["zhat"])
+    blocks = [(0, 0), (0, 31), (5, 7), (17, 30), (31, 0), (31, 31)]
+    n = _teacher_forced_check(arch, imgs[1], r["zhat"][1].cpu().numpy(), r["symbols"][1].cpu().numpy(),
+                              r["indexes"][1].cpu().numpy(), blocks)
+    assert n == len(blocks)
