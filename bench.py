@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpixels/s encode+decode of the block-level masked-conv codec (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), a batch of 32 synthetic
+768x768 frames per GPU.  One step = the reference's timed region of eval_model
+(agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
+rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
+GPU rANS decode).  Inputs are resident in HBM when the timed region starts.  Weights are the seeded
+synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
+checkpoints offline).
+
+Multi-GPU (torchrun, one process per GPU): every rank codes its own 32 frames (weak scaling); the only
+collectives are a barrier, a MAX of the step time and one all_gather of the per-image rate/distortion
+summary (RCCL over xGMI).
+
+Prints ONE JSON line on rank 0.  See DESIGN.md for the roofline definitions.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "learned-block-based-image-compression_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "Mpixels/s encode+decode, B8_lowrate N768M96, 768×768; bpp/PSNR vs ref"
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA (dense) peak
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+CONFIGS = {   # name -> (B, KS, N, M)
+    "B8_lowrate": (8, (3, 1, 1, 1), 768, 96),
+    "B8_highrate": (8, (3, 3, 1, 1), 1152, 128),
+    "B4_highrate": (4, (3, 3, 1, 1), 512, 96),
+    "B16_lowrate": (16, (3, 1, 1, 1), 1280, 192),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(arch, sd, H, W, budget_s):
+    """The oracle (numpy fp32 + C rANS, one thread) on a bounded sample: the first R block rows of one
+    frame, encode + decode; R chosen so the sample takes about `budget_s`."""
+    from threadpoolctl import threadpool_limits
+    from oracle import oracle as O
+    img = np.random.default_rng(0).integers(0, 256, (3, H, W), dtype=np.uint8).astype(np.float32) / 255.0 - 0.5
+    xb = O.image_to_blocks(img, arch.B)
+    Hb, Wb = xb.shape[:2]
+    with threadpool_limits(limits=1):
+        codec = O.OracleCodec(arch, sd)
+
+        def run(rows):
+            t0 = time.perf_counter()
+            out = codec.compress(xb, rows=rows)
+            codec.decompress(out["bytes"], Hb, Wb, rows=rows)
+            return time.perf_counter() - t0
+
+        t1 = run(1)
+        rows = int(max(1, min(Hb, math.floor(budget_s / max(t1, 1e-3)))))
+        t = run(rows) if rows > 1 else t1
+    px = rows * arch.B * W
+    return dict(value=px / t / 1e6, unit="Mpixels/s", cores=1, kind="port",
+                sample=f"oracle/oracle.py (numpy fp32, 1 thread, C rANS) encode+decode of the first {rows} of {Hb} "
+                       f"block rows of one {H}x{W} frame ({rows * Wb} blocks, {t:.1f} s); per-block cost is "
+                       f"content-independent, so the full frame extrapolates to {t * Hb / rows:.0f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
+    ap.add_argument("--size", type=int, default=768)
+    ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
+    ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=dev)
+
+    import types
+    from lbic.arch import Arch
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    from lbic.weights import synth_state_dict
+    from lbic.layout import image_to_blocks
+
+    B, KS, N, M = CONFIGS[args.config]
+    arch = Arch(B, KS, N, M)
+    H = W = args.size
+    Hb, Wb = H // B, W // B
+    cfg = types.SimpleNamespace(block_size=B, KS=list(KS), N=N, M=M, gpu_device=local)
+    sd = synth_state_dict(arch, 1337)
+    model = BlockBasedImgCompLossyNetv9(cfg, device=dev)
+    model.load_state_dict(sd)
+    model.update(force=True)
+
+    n = args.batch
+    frames = np.stack([image_to_blocks(np.random.default_rng(rank * n + k).integers(0, 256, (3, H, W), dtype=np.uint8)
+                                       .astype(np.float32) / 255.0 - 0.5, B) for k in range(n)])
+    xb = torch.from_numpy(frames).to(dev)
+    del frames
+
+    phase = dict(encode=0.0, entropy=0.0, decode=0.0)
+
+    def step(record=False):
+        t0 = time.perf_counter()
+        r = model.compress_batch(xb)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        streams = model.entropy_encode(r["symbols"], r["indexes"])
+        t2 = time.perf_counter()
+        z = model.decompress_batch(streams, Hb, Wb)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if record:
+            phase["encode"] += t1 - t0
+            phase["entropy"] += t2 - t1
+            phase["decode"] += t3 - t2
+        return r, streams, z
+
+    for i in range(args.warmup):
+        step()
+        log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    model.profile_begin(args.sample_every)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        r, streams, z = step(record=True)
+        log(f"[rank {rank}] step {i + 1}/{args.steps}: {time.perf_counter() - t0:.2f} s")
+    barrier()
+    dt = time.perf_counter() - t0
+    kstats = model.profile_end()
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # --- quality / consistency of the last step (outside the timed region)
+    bit_exact = bool(torch.equal(z, r["zhat"]))
+    sse = ((z - xb) ** 2).double().sum(dim=(1, 2, 3))
+    rec = torch.stack([torch.tensor([float(len(s)) for s in streams], dtype=torch.float64, device=dev), sse,
+                       torch.full((n,), float(H * W * 3), dtype=torch.float64, device=dev)], dim=1)
+    if dist:
+        allrec = [torch.empty_like(rec) for _ in range(world)]
+        torch.distributed.all_gather(allrec, rec)
+        rec = torch.cat(allrec)
+        ok = torch.tensor([1.0 if bit_exact else 0.0], device=dev)
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+        bit_exact = bool(ok.item() == 1.0)
+    rec = rec.cpu().numpy()
+    bpp = float(np.mean(rec[:, 0] * 8.0 / (H * W)))
+    mse = rec[:, 1] / rec[:, 2]
+    psnr = float(np.mean(-10 * np.log10(mse)))
+
+    if rank != 0:
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
+
+    ms_step = dt / args.steps * 1e3
+    px_total = world * n * H * W
+    value = px_total / (dt / args.steps) / 1e6
+
+    # --- roofline of the dominant kernel (sampled HIP events over the timed region)
+    roof = None
+    kernels = {}
+    if kstats:
+        for name, s in kstats.items():
+            avg = s["total_ms"] / max(s["launches"], 1)
+            kernels[name] = dict(launches_sampled=s["launches"], avg_us=round(avg * 1e3, 3),
+                                 total_ms_sampled=round(s["total_ms"], 3))
+        dom = max(kstats, key=lambda k: kstats[k]["total_ms"])
+        s = kstats[dom]
+        t_s = s["total_ms"] / 1e3
+        ai = s["flops"] / s["bytes"] if s["bytes"] else float("inf")
+        ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        if s["flops"] > 0 and ai >= ridge:
+            ach, peak, unit, bound = s["flops"] / t_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
+        else:
+            ach, peak, unit, bound = s["bytes"] / t_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+        roof = dict(kernel=dom, bound=bound, achieved=round(ach, 3), peak=peak, unit=unit,
+                    frac=round(ach / peak, 5), traffic=None,
+                    avg_launch_us=round(s["total_ms"] / s["launches"] * 1e3, 3),
+                    algorithmic_per_launch=dict(flops=s["flops"] / s["launches"], bytes=s["bytes"] / s["launches"]),
+                    arithmetic_intensity=round(ai, 2))
+        mfma_frac = sum(v["flops"] for v in kstats.values()) / (sum(v["total_ms"] for v in kstats.values()) / 1e3) \
+            / (PEAK_FP32_TFLOPS * 1e12)
+        roof["all_kernels_mfma_frac"] = round(mfma_frac, 5)
+    # whole-step algorithmic work
+    mac_enc, mac_dec = arch.live_macs_per_block()
+    step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
+    cpu = None
+    if args.cpu_budget > 0 and world == 1:
+        cpu = cpu_baseline(arch, sd, H, W, args.cpu_budget)
+
+    out = {
+        "metric": METRIC, "value": round(value, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: seeded uint8 noise frames, seeded synthetic weights (no checkpoints / Kodak offline)",
+        "config": {"workload": f"{args.config} N{N}M{M}, batch of {n} synthetic {H}x{W} frames per GPU, "
+                               "encode+decode in the reference bitstream format (one raster rANS stream per image)",
+                   "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
+                   "global_batch": n * world},
+        "roofline": roof, "cpu_baseline": cpu,
+        "quality": {"bpp": round(bpp, 5), "psnr_db": round(psnr, 3), "enc_dec_bit_exact": bit_exact},
+        "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
+        "step_algorithmic_tflop": round(step_flops / 1e12, 3),
+        "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
+        "kernels": kernels,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -99,6 +99,21 @@ const char *lbc_last_error(void);
  * total milliseconds of the encode and decode phases. */
 int lbc_last_timing(const lbc_model *m, double *enc_ms, double *dec_ms);
 
+/* Per-kernel HIP-event instrumentation (bench.py's roofline): while enabled, every `sample_every`-th
+ * wavefront / raster step brackets each kernel launch with a pair of events on the launch stream and
+ * records the launch's algorithmic FLOPs and bytes.  lbc_profile_end synchronises and returns one
+ * record per kernel (template instantiation). */
+typedef struct {
+    char name[40];
+    long long launches;   /* sampled launches */
+    double total_ms;      /* summed event-to-event durations */
+    double flops;         /* summed algorithmic FLOPs (2 * rows * K_live * N for a GEMM) */
+    double bytes;         /* summed algorithmic bytes (weights + A rows + outputs read/written once) */
+} lbc_kernel_stat;
+
+int lbc_profile_begin(lbc_model *m, int sample_every);
+int lbc_profile_end(lbc_model *m, lbc_kernel_stat *out, int max_out, int *n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,18 @@ struct Layer {
     int K = 0, N = 0, NB16 = 0;
 };
 
+// sampled per-kernel event timing (lbc_profile_begin / lbc_profile_end)
+struct Prof {
+    int sample_every = 0;
+    bool active = false;          // current step is sampled
+    struct Rec { int cls; int ev; double flops, bytes; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    int used = 0;
+};
+static const char* kKernelNames[] = {"k_gemm<32,16,8>", "k_gemm<64,32,4>", "k_rans_decode", "k_copy_interior"};
+static thread_local Prof* g_prof = nullptr;
+
 struct HostT {
     std::vector<float> v;
     std::vector<int64_t> shape;
@@ -100,6 +112,7 @@ struct lbc_model {
     DevBuf words, word_base, word_count, st_x, st_ptr, st_status;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool enc_timed = false, dec_timed = false;
+    Prof prof;
 };
 
 namespace {
@@ -266,6 +279,32 @@ int prepare_device(lbc_model* m) {
     return LBC_OK;
 }
 
+int prof_event(Prof* p, hipStream_t s) {
+    if (p->used == (int)p->pool.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        p->pool.push_back(e);
+    }
+    HIPCHK(hipEventRecord(p->pool[p->used], s));
+    return p->used++;
+}
+
+// launch a GEMM; in a sampled step bracket it with events and record its algorithmic work
+int gemm(const GemmArgs& g, hipStream_t s, int k_live = -1) {
+    Prof* p = g_prof;
+    if (!p || !p->active) return launch_gemm(g, s);
+    const int e0 = prof_event(p, s);
+    int cls = 0;
+    int rc = launch_gemm(g, s, &cls);
+    if (rc) return rc;
+    prof_event(p, s);
+    const double K = k_live > 0 ? k_live : g.K;
+    const double flops = 2.0 * g.M * K * g.N;
+    const double bytes = 4.0 * (K * g.N + (double)g.M * K + (double)g.M * g.N * (g.square_a ? 2 : 1));
+    p->recs.push_back({cls, e0, flops, bytes});
+    return LBC_OK;
+}
+
 GemmArgs base_args(lbc_model* m, const int4* blocks, int rows, const float* x, int n_img, int Hb, int Wb) {
     GemmArgs g{};
     g.M = rows;
@@ -314,7 +353,7 @@ int run_dense(GemmArgs g, const Layer& L, const float* in, int ld_in, int epi, f
     g.square_a = 0;
     set_layer(g, L, epi, out, ldo);
     seg_dense(g, in, ld_in, 0, L.K);
-    return launch_gemm(g, s);
+    return gemm(g, s);
 }
 
 // ld: row stride of `in` and `out` (the padded activation width)
@@ -325,7 +364,7 @@ int run_gdn(GemmArgs g, const Layer& L, const float* in, int ld, bool inverse, f
     g.square_a = 1;
     g.gx = in;
     g.ldx = ld;
-    return launch_gemm(g, s);
+    return gemm(g, s);
 }
 
 // context net (get_meanscale_fast, net:389-398) for the rows of `g`; the last layer's epilogue is
@@ -344,7 +383,7 @@ int run_ctx(lbc_model* m, GemmArgs g, bool with_idx, hipStream_t s) {
         }
         set_layer(c, m->ctx0, EPI_LEAKY, m->a_ctx0.as<float>(), m->C1P);
         segs_ztaps(c, m->Cx);
-        if ((rc = launch_gemm(c, s))) return rc;
+        if ((rc = gemm(c, s))) return rc;
     }
     if ((rc = run_dense(g, m->ctx1, m->a_ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, m->a_ctx1.as<float>(), m->C2P, s)))
         return rc;
@@ -366,7 +405,7 @@ int run_dec(lbc_model* m, GemmArgs g, hipStream_t s) {
         set_layer(c, m->dec0, EPI_BIAS, m->a_d0.as<float>(), m->NP);
         segs_ztaps(c, m->Cx);
         seg_dense(c, m->a_yq.as<float>(), m->M, 4 * m->Cx, 4 * m->Cx + m->M);
-        if ((rc = launch_gemm(c, s))) return rc;
+        if ((rc = gemm(c, s))) return rc;
     }
     float *d0 = m->a_d0.as<float>(), *d1 = m->a_d1.as<float>();
     const int W = m->NP;
@@ -390,7 +429,7 @@ int run_enc(lbc_model* m, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, h
         segs_ztaps(c, m->Cx);
         Seg& sx = c.seg[c.nseg++];
         sx = Seg{nullptr, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
-        if ((rc = launch_gemm(c, s))) return rc;
+        if ((rc = gemm(c, s))) return rc;
     }
     const int W = m->NP;
     if ((rc = run_gdn(g, m->g0, e0, W, false, e1, s))) return rc;
@@ -555,13 +594,17 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
     HIPCHK(hipEventRecord(m->ev[0], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
     const int4* blocks = m->blocks_enc.as<int4>();
+    g_prof = &m->prof;
     for (size_t t = 0; t < m->step_off.size(); ++t) {
+        m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
         const int rows = m->step_cnt[t];
         GemmArgs g = base_args(m, blocks + m->step_off[t], rows, x_dev, n_img, Hb, Wb);
         if ((rc = run_ctx(m, g, false, s))) return rc;
         if ((rc = run_enc(m, g, sym_dev, idx_dev, bits_dev, s))) return rc;
         if ((rc = run_dec(m, g, s))) return rc;
     }
+    m->prof.active = false;
+    g_prof = nullptr;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[1], s));
     m->enc_timed = true;
@@ -638,14 +681,27 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     ra.yq = m->a_yq.as<float>();
     ra.ldy = m->M;
     ra.rows = n_img;
+    g_prof = &m->prof;
     for (int st = 0; st < Hb * Wb; ++st) {
+        m->prof.active = m->prof.sample_every > 0 && (st % m->prof.sample_every) == 0;
         const int4* blocks = m->blocks_dec.as<int4>() + (size_t)st * n_img;
         GemmArgs g = base_args(m, blocks, n_img, nullptr, n_img, Hb, Wb);
         if ((rc = run_ctx(m, g, true, s))) return rc;
         ra.blocks = blocks;
-        if ((rc = launch_rans_decode(ra, s))) return rc;
+        if (m->prof.active) {
+            const int e0 = prof_event(&m->prof, s);
+            if ((rc = launch_rans_decode(ra, s))) return rc;
+            prof_event(&m->prof, s);
+            // algorithmic bytes: the CDF tables staged into LDS + idx/mean in + y_qnt out
+            const double b = (double)m->total16 * 2 * n_img + 12.0 * n_img * m->M;
+            m->prof.recs.push_back({2, e0, 0.0, b});
+        } else if ((rc = launch_rans_decode(ra, s))) {
+            return rc;
+        }
         if ((rc = run_dec(m, g, s))) return rc;
     }
+    m->prof.active = false;
+    g_prof = nullptr;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[3], s));
     m->dec_timed = true;
@@ -654,6 +710,39 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     HIPCHK(hipStreamSynchronize(s));
     for (int i = 0; i < n_img; ++i)
         if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream for image " + std::to_string(i));
+    return LBC_OK;
+}
+
+int lbc_profile_begin(lbc_model* m, int sample_every) {
+    if (!m || sample_every < 0) return set_error(LBC_E_ARG, "bad argument");
+    m->prof.sample_every = sample_every;
+    m->prof.recs.clear();
+    m->prof.used = 0;
+    return LBC_OK;
+}
+
+int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out) {
+    if (!m || !out || !n_out) return set_error(LBC_E_ARG, "null argument");
+    Prof& p = m->prof;
+    lbc_kernel_stat acc[4];
+    std::memset(acc, 0, sizeof(acc));
+    for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", kKernelNames[c]);
+    if (!p.recs.empty()) HIPCHK(hipEventSynchronize(p.pool[p.used - 1]));
+    for (const auto& r : p.recs) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, p.pool[r.ev], p.pool[r.ev + 1]));
+        acc[r.cls].launches += 1;
+        acc[r.cls].total_ms += ms;
+        acc[r.cls].flops += r.flops;
+        acc[r.cls].bytes += r.bytes;
+    }
+    int n = 0;
+    for (int c = 0; c < 4 && n < max_out; ++c)
+        if (acc[c].launches) out[n++] = acc[c];
+    *n_out = n;
+    p.sample_every = 0;
+    p.recs.clear();
+    p.used = 0;
     return LBC_OK;
 }
 

@@ -79,7 +79,7 @@ struct RansArgs {
     int rows;
 };
 
-int launch_gemm(const GemmArgs& g, hipStream_t s);
+int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = <32,16,8>, 1 = <64,32,4>
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
 

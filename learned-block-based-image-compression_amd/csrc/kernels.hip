@@ -193,10 +193,14 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm launch failed");
 }
 
-int launch_gemm(const GemmArgs& g, hipStream_t s) {
+int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id) {
     if (g.M <= 0) return LBC_OK;
     if (g.K % 16 || g.K < 16) return set_error(LBC_E_ARG, "GEMM K must be a positive multiple of 16");
-    if (g.M <= 64) return launch_cfg<32, 16, 8>(g, s);
+    if (g.M <= 64) {
+        if (cfg_id) *cfg_id = 0;
+        return launch_cfg<32, 16, 8>(g, s);
+    }
+    if (cfg_id) *cfg_id = 1;
     return launch_cfg<64, 32, 4>(g, s);
 }
 

@@ -14,6 +14,11 @@ LIB_PATH = os.path.join(HERE, "liblbic.so")
 LBC_E_NOT_UPDATED = -4
 
 
+class LbcKernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_longlong), ("total_ms", ctypes.c_double),
+                ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
 class LbcConfig(ctypes.Structure):
     _fields_ = [("block_size", ctypes.c_int), ("ks", ctypes.c_int * 4), ("n", ctypes.c_int),
                 ("m", ctypes.c_int), ("device", ctypes.c_int)]
@@ -36,6 +41,9 @@ _SIGS = {
     "lbc_free": ([_P], None),
     "lbc_last_error": ([], ctypes.c_char_p),
     "lbc_last_timing": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "lbc_profile_begin": ([_P, ctypes.c_int], ctypes.c_int),
+    "lbc_profile_end": ([_P, ctypes.POINTER(LbcKernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
+                        ctypes.c_int),
 }
 EXPORTS = tuple(_SIGS)
 

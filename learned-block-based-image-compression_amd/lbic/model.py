@@ -44,6 +44,8 @@ class BlockBasedImgCompLossyNetv9:
         self._h = h
         self._tables_uploaded = False
         self.training = False
+        self._pool = None
+        self._pool_workers = 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -145,20 +147,32 @@ class BlockBasedImgCompLossyNetv9:
                                          ctypes.c_void_p(stream)))
         return dict(zhat=zhat, symbols=sym, indexes=idx, bits=bits)
 
-    def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor) -> List[bytes]:
-        """BufferedRansEncoder per image (host C++), symbols/indexes [n, L] (any device)."""
+    def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor, workers: int = 0) -> List[bytes]:
+        """BufferedRansEncoder per image (host C++, one stream per image as in the reference),
+        symbols/indexes [n, L] (any device).  Images are coded on parallel host threads (ctypes drops the
+        GIL during the call)."""
         s = symbols.to("cpu", torch.int32).contiguous().numpy()
         i = indexes.to("cpu", torch.int32).contiguous().numpy()
-        out = []
         L = _lib.lib()
-        for k in range(s.shape[0]):
+
+        def one(k):
             p = ctypes.c_void_p()
             ln = ctypes.c_size_t()
             _lib.check(L.lbc_rans_encode(self._h, _lib.ptr(s[k]), _lib.ptr(i[k]), s.shape[1], ctypes.byref(p),
                                          ctypes.byref(ln)))
-            out.append(ctypes.string_at(p, ln.value))
+            b = ctypes.string_at(p, ln.value)
             L.lbc_free(p)
-        return out
+            return b
+
+        n = s.shape[0]
+        workers = workers or min(n, 16)
+        if n == 1 or workers <= 1:
+            return [one(k) for k in range(n)]
+        if self._pool is None or self._pool_workers != workers:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=workers)
+            self._pool_workers = workers
+        return list(self._pool.map(one, range(n)))
 
     def decompress_batch(self, streams: Sequence[bytes], Hb: int, Wb: int) -> torch.Tensor:
         """Decode n bitstreams of Hb x Wb blocks on the GPU -> zhat [n, Hb, Wb, 3B^2]."""
@@ -171,6 +185,18 @@ class BlockBasedImgCompLossyNetv9:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(_lib.lib().lbc_decode(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
+
+    def profile_begin(self, sample_every: int):
+        """Sample every n-th step's kernels with HIP events (lbc_profile_begin)."""
+        _lib.check(_lib.lib().lbc_profile_begin(self._h, int(sample_every)))
+
+    def profile_end(self):
+        """-> {kernel name: dict(launches, total_ms, flops, bytes)} for the sampled launches."""
+        arr = (_lib.LbcKernelStat * 8)()
+        n = ctypes.c_int()
+        _lib.check(_lib.lib().lbc_profile_end(self._h, arr, 8, ctypes.byref(n)))
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms, flops=arr[i].flops,
+                                           bytes=arr[i].bytes) for i in range(n.value)}
 
     def last_timing(self):
         e, d = ctypes.c_double(), ctypes.c_double()
