@@ -136,6 +136,8 @@ def main():
             phase["decode"] += t3 - t2
         return r, streams, z
 
+    # sampling is part of the captured graphs: enable it before the warmup builds them
+    model.profile_begin(args.sample_every)
     for i in range(args.warmup):
         step()
         log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
@@ -145,7 +147,6 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
-    model.profile_begin(args.sample_every)
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -185,7 +186,8 @@ def main():
     px_total = world * n * H * W
     value = px_total / (dt / args.steps) / 1e6
 
-    # --- roofline of the dominant kernel (sampled HIP events over the timed region)
+    # --- roofline of the dominant kernel: launch spans of the sampled launches (in-kernel stamps on the
+    #     GPU's 100 MHz clock, last replay of each graph in the timed region)
     roof = None
     kernels = {}
     if kstats:

@@ -65,16 +65,23 @@ struct Layer {
     int K = 0, N = 0, NB16 = 0;
 };
 
-// sampled per-kernel event timing (lbc_profile_begin / lbc_profile_end)
+// sampled per-kernel timing (lbc_profile_begin / lbc_profile_end): sampled launches stamp their span
+// into a device slot {max(~start), max(end)}; one slot range per graph, zeroed at every replay
+constexpr int kSlotsPerRange = 4096;
+constexpr int kSlotU64 = 16;      // 8 XCDs x {max(~start), max(end)}
 struct Prof {
     int sample_every = 0;
     bool active = false;          // current step is sampled
-    struct Rec { int cls; int ev; double flops, bytes; };
+    struct Rec { int cls; int slot; double flops, bytes; };
     std::vector<Rec> recs;
-    std::vector<hipEvent_t> pool;
-    int used = 0;
+    unsigned long long* slots = nullptr;   // device, kLanes + 1 ranges
+    int range = 0, next = 0;               // slot allocation inside the range being captured
+    unsigned long long* take() {
+        if (!slots || next >= kSlotsPerRange) return nullptr;
+        return slots + kSlotU64 * ((size_t)range * kSlotsPerRange + next++);
+    }
 };
-static const char* kKernelNames[] = {"k_gemm<32,16,8>", "k_gemm<64,32,4>", "k_rans_decode", "k_copy_interior"};
+static const char* kKernelNames[] = {"k_gemm<16,16,8>", "k_gemm<64,32,4>", "k_rans_decode", "k_copy_interior"};
 static thread_local Prof* g_prof = nullptr;
 
 struct HostT {
@@ -83,6 +90,14 @@ struct HostT {
 };
 
 inline int pad16(int x) { return (x + 15) & ~15; }
+
+// A "lane" = one HIP stream + its own step workspace.  The encoder runs on lane 0 (the caller's
+// stream); the decoder splits the images into kLanes groups whose raster chains run concurrently.
+constexpr int kLanes = 4;
+struct Work {
+    int rows = 0;
+    DevBuf ctx0, ctx1, ctx2, ksi, e0, e1, yq, d0, d1, idx;
+};
 
 static const int TAPS_A[4][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}};       // masked_conv2d.py:9-17 'A'
 static const int TAPS_B[5][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0}};  // 'B' adds the centre
@@ -107,12 +122,22 @@ struct lbc_model {
     bool tabs_dirty = false;
     // per-shape workspace
     int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
-    DevBuf zpad, blocks_enc, blocks_dec, a_ctx0, a_ctx1, a_ctx2, a_ksi, a_e0, a_e1, a_yq, a_d0, a_d1, a_idx;
+    DevBuf zpad, blocks_enc, blocks_dec;
+    Work lane[kLanes];
+    hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     std::vector<int> step_off, step_cnt;
     DevBuf words, word_base, word_count, st_x, st_ptr, st_status;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool enc_timed = false, dec_timed = false;
     Prof prof;
+    // HIP graphs: the whole encoder wavefront (one replay per call) and, per decoder lane, one block row
+    // (replayed Hb times; kernels take the row from a device counter)
+    hipGraphExec_t enc_exec = nullptr;
+    std::vector<hipGraphExec_t> dec_exec;
+    std::vector<long long> enc_key, dec_key;
+    DevBuf x_in, sym_buf, idx_buf, bits_buf, ctr;
+    hipStream_t cap = nullptr;
 };
 
 namespace {
@@ -241,21 +266,30 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
     std::vector<int4> dec((size_t)Hb * Wb * n_img);
     for (int s = 0; s < Hb * Wb; ++s)
         for (int img = 0; img < n_img; ++img) dec[(size_t)s * n_img + img] = make_int4(img, s / Wb, s % Wb, 0);
+    // the GEMM kernel addresses rows with 32-bit element offsets
+    if ((double)n_img * (Hb + 2) * (Wb + 4) * m->Cx >= 2147483647.0 ||
+        (double)mmax * m->P * std::max({m->C1P, m->NP, m->C2P}) * 5 >= 2147483647.0)
+        return set_error(LBC_E_ARG, "frame batch too large for 32-bit offsets; split the batch");
     int rc;
     if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4)))) return rc;
     if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4)))) return rc;
-    const size_t rows = (size_t)mmax;
     const size_t F = sizeof(float);
     if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
-    // activation widths are padded to 16 columns; the pad columns are zeroed once and never written,
-    // so GEMMs can run K over whole 16-wide k-blocks (their weights are zero there too)
-    DevBuf* bufs[] = {&m->a_ctx0, &m->a_ctx1, &m->a_ctx2, &m->a_ksi, &m->a_e0, &m->a_e1,
-                      &m->a_d0, &m->a_d1, &m->a_yq, &m->a_idx};
-    const size_t widths[] = {(size_t)m->P * m->C1P, (size_t)m->C2P, (size_t)m->C3P, (size_t)m->C4, (size_t)m->NP,
-                             (size_t)m->NP, (size_t)m->NP, (size_t)m->NP, (size_t)m->M, (size_t)m->M};
-    for (int i = 0; i < 10; ++i) {
-        if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
-        HIPCHK(hipMemset(bufs[i]->p, 0, rows * widths[i] * F));
+    const int gmax = n_img;      // a decoder lane may get every image (lane count is chosen per call)
+    for (int l = 0; l < kLanes; ++l) {
+        Work& w = m->lane[l];
+        const size_t rows = (size_t)(l == 0 ? mmax : gmax);
+        w.rows = (int)rows;
+        // activation widths are padded to 16 columns; the pad columns are zeroed once and never
+        // written, so GEMMs can run K over whole 16-wide k-blocks (their weights are zero there too)
+        DevBuf* bufs[] = {&w.ctx0, &w.ctx1, &w.ctx2, &w.ksi, &w.e0, &w.e1, &w.d0, &w.d1, &w.yq, &w.idx};
+        const size_t widths[] = {(size_t)m->P * m->C1P, (size_t)m->C2P, (size_t)m->C3P, (size_t)m->C4, (size_t)m->NP,
+                                 (size_t)m->NP, (size_t)m->NP, (size_t)m->NP, (size_t)m->M, (size_t)m->M};
+        for (int i = 0; i < 10; ++i) {
+            if (l > 0 && (i == 4 || i == 5)) continue;   // encoder-only buffers
+            if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
+            HIPCHK(hipMemset(bufs[i]->p, 0, rows * widths[i] * F));
+        }
     }
     m->Mmax = mmax;
     m->ws_n = n_img;
@@ -267,8 +301,12 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
 // first device use: events and the entropy tables (host copies made by lbc_set_entropy_tables)
 int prepare_device(lbc_model* m) {
     HIPCHK(hipSetDevice(m->cfg.device));
-    if (!m->ev[0])
+    if (!m->ev[0]) {
         for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
+        for (auto& e : m->lev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& st : m->lstream) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
+    }
     if (m->tabs_dirty) {
         int rc;
         if ((rc = dev_upload(m->table_dev, m->tabs.table.data(), 64 * sizeof(float)))) return rc;
@@ -279,29 +317,37 @@ int prepare_device(lbc_model* m) {
     return LBC_OK;
 }
 
-int prof_event(Prof* p, hipStream_t s) {
-    if (p->used == (int)p->pool.size()) {
-        hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
-        p->pool.push_back(e);
-    }
-    HIPCHK(hipEventRecord(p->pool[p->used], s));
-    return p->used++;
+void drop_recs(Prof& p, int r) {
+    std::vector<Prof::Rec> keep;
+    for (const auto& x : p.recs)
+        if (x.slot / kSlotsPerRange != r) keep.push_back(x);
+    p.recs.swap(keep);
 }
 
-// launch a GEMM; in a sampled step bracket it with events and record its algorithmic work
-int gemm(const GemmArgs& g, hipStream_t s, int k_live = -1) {
+// start capturing sampled launches into slot range r: the range is zeroed by the graph's first node
+int prof_range_begin(Prof* p, int r, hipStream_t s) {
+    p->range = r;
+    p->next = 0;
+    if (p->sample_every && p->slots)
+        HIPCHK(hipMemsetAsync(p->slots + kSlotU64 * (size_t)r * kSlotsPerRange, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange, s));
+    return LBC_OK;
+}
+
+// launch a GEMM; in a sampled step give it a timing slot and record its algorithmic work
+int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     Prof* p = g_prof;
-    if (!p || !p->active) return launch_gemm(g, s);
-    const int e0 = prof_event(p, s);
+    if (!p || !p->active) return launch_gemm(g0, s);
+    GemmArgs g = g0;
+    g.ts = p->take();
+    if (!g.ts) return launch_gemm(g0, s);
+    const int slot = (int)((g.ts - p->slots) / kSlotU64);
     int cls = 0;
     int rc = launch_gemm(g, s, &cls);
     if (rc) return rc;
-    prof_event(p, s);
     const double K = k_live > 0 ? k_live : g.K;
     const double flops = 2.0 * g.M * K * g.N;
     const double bytes = 4.0 * (K * g.N + (double)g.M * K + (double)g.M * g.N * (g.square_a ? 2 : 1));
-    p->recs.push_back({cls, e0, flops, bytes});
+    p->recs.push_back({cls, slot, flops, bytes});
     return LBC_OK;
 }
 
@@ -344,7 +390,7 @@ void seg_dense(GemmArgs& g, const float* base, int ld, int k0, int k1) {
 void segs_ztaps(GemmArgs& g, int Cx) {
     for (int t = 0; t < 4; ++t) {
         Seg& s = g.seg[g.nseg++];
-        s = Seg{nullptr, SEG_ZTAP, 0, TAPS_A[t][0], TAPS_A[t][1], t * Cx, (t + 1) * Cx};
+        s = Seg{g.geo.zpad, SEG_ZTAP, 0, TAPS_A[t][0], TAPS_A[t][1], t * Cx, (t + 1) * Cx};
     }
 }
 
@@ -369,7 +415,7 @@ int run_gdn(GemmArgs g, const Layer& L, const float* in, int ld, bool inverse, f
 
 // context net (get_meanscale_fast, net:389-398) for the rows of `g`; the last layer's epilogue is
 // plain (encode) or also emits the scale indexes (decode).
-int run_ctx(lbc_model* m, GemmArgs g, bool with_idx, hipStream_t s) {
+int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s) {
     int rc;
     {
         GemmArgs c = g;
@@ -381,33 +427,33 @@ int run_ctx(lbc_model* m, GemmArgs g, bool with_idx, hipStream_t s) {
             c.pos_dy[p] = m->P == 1 ? 0 : TAPS_B[p][0];
             c.pos_dx[p] = m->P == 1 ? 0 : TAPS_B[p][1];
         }
-        set_layer(c, m->ctx0, EPI_LEAKY, m->a_ctx0.as<float>(), m->C1P);
+        set_layer(c, m->ctx0, EPI_LEAKY, w.ctx0.as<float>(), m->C1P);
         segs_ztaps(c, m->Cx);
         if ((rc = gemm(c, s))) return rc;
     }
-    if ((rc = run_dense(g, m->ctx1, m->a_ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, m->a_ctx1.as<float>(), m->C2P, s)))
+    if ((rc = run_dense(g, m->ctx1, w.ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, w.ctx1.as<float>(), m->C2P, s)))
         return rc;
-    if ((rc = run_dense(g, m->ctx2, m->a_ctx1.as<float>(), m->C2P, EPI_LEAKY, m->a_ctx2.as<float>(), m->C3P, s)))
+    if ((rc = run_dense(g, m->ctx2, w.ctx1.as<float>(), m->C2P, EPI_LEAKY, w.ctx2.as<float>(), m->C3P, s)))
         return rc;
     GemmArgs c = g;
-    c.idx = m->a_idx.as<int32_t>();
-    return run_dense(c, m->ctx3, m->a_ctx2.as<float>(), m->C3P, with_idx ? EPI_CTXIDX : EPI_BIAS, m->a_ksi.as<float>(),
+    c.idx = w.idx.as<int32_t>();
+    return run_dense(c, m->ctx3, w.ctx2.as<float>(), m->C3P, with_idx ? EPI_CTXIDX : EPI_BIAS, w.ksi.as<float>(),
                      m->C4, s);
 }
 
 // decoder transform (inverse_prtr_fast, net:384-387) + clamp + write-back into zpad (net:357)
-int run_dec(lbc_model* m, GemmArgs g, hipStream_t s) {
+int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s) {
     int rc;
     {
         GemmArgs c = g;
         c.nseg = 0;
         c.square_a = 0;
-        set_layer(c, m->dec0, EPI_BIAS, m->a_d0.as<float>(), m->NP);
+        set_layer(c, m->dec0, EPI_BIAS, w.d0.as<float>(), m->NP);
         segs_ztaps(c, m->Cx);
-        seg_dense(c, m->a_yq.as<float>(), m->M, 4 * m->Cx, 4 * m->Cx + m->M);
+        seg_dense(c, w.yq.as<float>(), m->M, 4 * m->Cx, 4 * m->Cx + m->M);
         if ((rc = gemm(c, s))) return rc;
     }
-    float *d0 = m->a_d0.as<float>(), *d1 = m->a_d1.as<float>();
+    float *d0 = w.d0.as<float>(), *d1 = w.d1.as<float>();
     const int W = m->NP;
     if ((rc = run_gdn(g, m->ig0, d0, W, true, d1, s))) return rc;
     if ((rc = run_dense(g, m->d1, d1, W, EPI_BIAS, d0, W, s))) return rc;
@@ -418,9 +464,9 @@ int run_dec(lbc_model* m, GemmArgs g, hipStream_t s) {
 }
 
 // encoder transform (forward_prtr_fast, net:379-382) + quantize epilogue
-int run_enc(lbc_model* m, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, hipStream_t s) {
+int run_enc(lbc_model* m, Work& w, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, hipStream_t s) {
     int rc;
-    float *e0 = m->a_e0.as<float>(), *e1 = m->a_e1.as<float>();
+    float *e0 = w.e0.as<float>(), *e1 = w.e1.as<float>();
     {
         GemmArgs c = g;
         c.nseg = 0;
@@ -428,7 +474,7 @@ int run_enc(lbc_model* m, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, h
         set_layer(c, m->enc0, EPI_BIAS, e0, m->NP);
         segs_ztaps(c, m->Cx);
         Seg& sx = c.seg[c.nseg++];
-        sx = Seg{nullptr, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
+        sx = Seg{c.geo.x, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
         if ((rc = gemm(c, s))) return rc;
     }
     const int W = m->NP;
@@ -438,12 +484,12 @@ int run_enc(lbc_model* m, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, h
     if ((rc = run_dense(g, m->e2, e1, W, EPI_BIAS, e0, W, s))) return rc;
     if ((rc = run_gdn(g, m->g2, e0, W, false, e1, s))) return rc;
     GemmArgs c = g;
-    c.ksi = m->a_ksi.as<float>();
+    c.ksi = w.ksi.as<float>();
     c.ldk = m->C4;
     c.sym = sym;
     c.idx = idx;
     c.bits = bits;
-    return run_dense(c, m->e3, e1, W, EPI_QUANT, m->a_yq.as<float>(), m->M, s);
+    return run_dense(c, m->e3, e1, W, EPI_QUANT, w.yq.as<float>(), m->M, s);
 }
 
 }  // namespace
@@ -484,6 +530,14 @@ void lbc_destroy(lbc_model* m) {
     if (!m) return;
     for (auto& e : m->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : m->lev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& st : m->lstream)
+        if (st) (void)hipStreamDestroy(st);
+    if (m->prof.slots) (void)hipFree(m->prof.slots);
+    if (m->enc_exec) (void)hipGraphExecDestroy(m->enc_exec);
+    for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
+    if (m->cap) (void)hipStreamDestroy(m->cap);
     delete m;
 }
 
@@ -571,7 +625,7 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
         }
         c16.push_back(0);   // slot of the implicit final 2^16
     }
-    if (c16.size() & 1) c16.push_back(0);
+    while (c16.size() & 7) c16.push_back(0);   // 16-byte granules for the LDS staging loads
     if (c16.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
     m->total16 = (int)c16.size();
     m->c16_host = std::move(c16);
@@ -591,21 +645,50 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
     int rc;
     if ((rc = prepare_device(m))) return rc;
     if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
-    HIPCHK(hipEventRecord(m->ev[0], s));
-    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
-    const int4* blocks = m->blocks_enc.as<int4>();
-    g_prof = &m->prof;
-    for (size_t t = 0; t < m->step_off.size(); ++t) {
-        m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
-        const int rows = m->step_cnt[t];
-        GemmArgs g = base_args(m, blocks + m->step_off[t], rows, x_dev, n_img, Hb, Wb);
-        if ((rc = run_ctx(m, g, false, s))) return rc;
-        if ((rc = run_enc(m, g, sym_dev, idx_dev, bits_dev, s))) return rc;
-        if ((rc = run_dec(m, g, s))) return rc;
+    const size_t nx = (size_t)n_img * Hb * Wb * m->Cx, nsym = (size_t)n_img * Hb * Wb * m->M;
+    if ((rc = m->x_in.alloc(nx * 4)) || (rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4)) ||
+        (rc = m->bits_buf.alloc(nsym * 4)))
+        return rc;
+    // the graph works on library-owned buffers only, so it survives new caller tensors
+    const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->x_in.p, (long long)m->zpad.p,
+                                        (long long)m->sym_buf.p, (long long)m->lane[0].ctx0.p,
+                                        (long long)m->table_dev.p, m->prof.sample_every};
+    if (!m->enc_exec || key != m->enc_key) {
+        if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
+        HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
+        int crc = prof_range_begin(&m->prof, 0, m->cap);
+        drop_recs(m->prof, 0);
+        const int4* blocks = m->blocks_enc.as<int4>();
+        g_prof = &m->prof;
+        for (size_t t = 0; t < m->step_off.size(); ++t)
+            if (m->step_cnt[t] > m->lane[0].rows) crc = set_error(LBC_E_STATE, "encoder workspace too small");
+        for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
+            m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
+            GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), n_img, Hb, Wb);
+            if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap);
+            if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
+                                    m->bits_buf.as<float>(), m->cap);
+            if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
+        }
+        m->prof.active = false;
+        g_prof = nullptr;
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(m->cap, &graph);
+        if (crc) { if (graph) (void)hipGraphDestroy(graph); return crc; }
+        if (e != hipSuccess) return set_error(LBC_E_HIP, std::string("encoder capture: ") + hipGetErrorString(e));
+        const hipError_t ei = hipGraphInstantiate(&m->enc_exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return set_error(LBC_E_HIP, std::string("encoder instantiate: ") + hipGetErrorString(ei));
+        m->enc_key = key;
     }
-    m->prof.active = false;
-    g_prof = nullptr;
+    HIPCHK(hipEventRecord(m->ev[0], s));
+    HIPCHK(hipMemcpyAsync(m->x_in.p, x_dev, nx * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    HIPCHK(hipGraphLaunch(m->enc_exec, s));
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
+    HIPCHK(hipMemcpyAsync(sym_dev, m->sym_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(idx_dev, m->idx_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
+    if (bits_dev) HIPCHK(hipMemcpyAsync(bits_dev, m->bits_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(m->ev[1], s));
     m->enc_timed = true;
     return LBC_OK;
@@ -655,7 +738,9 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     }
     std::vector<uint8_t> cat(total);
     for (int i = 0, off = 0; i < n_img; off += (int)lens[i], ++i) std::memcpy(cat.data() + off, streams[i], lens[i]);
-    if ((rc = dev_upload(m->words, cat.data(), cat.size()))) return rc;
+    // keep the stream buffer (baked into the decoder graphs) stable across calls: grow with headroom
+    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
+    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
     if ((rc = dev_upload(m->word_base, base.data(), base.size() * sizeof(long long)))) return rc;
     if ((rc = dev_upload(m->word_count, cnt.data(), cnt.size() * sizeof(int)))) return rc;
     if ((rc = dev_upload(m->st_x, x0.data(), x0.size() * sizeof(unsigned long long)))) return rc;
@@ -664,41 +749,90 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     HIPCHK(hipMemsetAsync(m->st_status.p, 0, n_img * sizeof(int), s));
     HIPCHK(hipEventRecord(m->ev[2], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
-    RansArgs ra{};
-    ra.cdf16 = m->cdf16_dev.as<uint16_t>();
-    ra.tmeta = m->tmeta_dev.as<int>();
-    ra.total16 = m->total16;
-    ra.words = m->words.as<uint32_t>();
-    ra.word_base = m->word_base.as<long long>();
-    ra.word_count = m->word_count.as<int>();
-    ra.state_x = m->st_x.as<unsigned long long>();
-    ra.state_ptr = m->st_ptr.as<int>();
-    ra.status = m->st_status.as<int>();
-    ra.idx = m->a_idx.as<int32_t>();
-    ra.ksi = m->a_ksi.as<float>();
-    ra.ldk = m->C4;
-    ra.Mlat = m->M;
-    ra.yq = m->a_yq.as<float>();
-    ra.ldy = m->M;
-    ra.rows = n_img;
-    g_prof = &m->prof;
-    for (int st = 0; st < Hb * Wb; ++st) {
-        m->prof.active = m->prof.sample_every > 0 && (st % m->prof.sample_every) == 0;
-        const int4* blocks = m->blocks_dec.as<int4>() + (size_t)st * n_img;
-        GemmArgs g = base_args(m, blocks, n_img, nullptr, n_img, Hb, Wb);
-        if ((rc = run_ctx(m, g, true, s))) return rc;
-        ra.blocks = blocks;
-        if (m->prof.active) {
-            const int e0 = prof_event(&m->prof, s);
-            if ((rc = launch_rans_decode(ra, s))) return rc;
-            prof_event(&m->prof, s);
-            // algorithmic bytes: the CDF tables staged into LDS + idx/mean in + y_qnt out
-            const double b = (double)m->total16 * 2 * n_img + 12.0 * n_img * m->M;
-            m->prof.recs.push_back({2, e0, 0.0, b});
-        } else if ((rc = launch_rans_decode(ra, s))) {
-            return rc;
+    // image groups -> lanes: every lane runs its own raster chain on its own stream, so the small
+    // per-step kernels of different groups fill the GPU side by side.  Each lane's block row (Wb raster
+    // steps, 13 launches each) is one captured HIP graph replayed Hb times: its kernels read the row
+    // from the lane's device counter, which the graph's last node advances.
+    // one lane by default: on ROCm 7.2 several streams' graphs did not overlap usefully
+    int G = 1;
+    if (const char* e = getenv("LBIC_DEC_LANES")) G = std::max(1, std::min(std::min(kLanes, n_img), atoi(e)));
+    int g0[kLanes + 1];
+    for (int l = 0; l <= G; ++l) g0[l] = l * n_img / G;
+    if ((rc = m->ctr.alloc(kLanes * sizeof(int)))) return rc;
+    const std::vector<long long> key = {n_img, Hb, Wb, G, (long long)m->words.p, (long long)m->zpad.p,
+                                        (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
+                                        (long long)m->st_x.p, m->prof.sample_every};
+    if ((int)m->dec_exec.size() != G || key != m->dec_key) {
+        for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
+        m->dec_exec.clear();
+        g_prof = &m->prof;
+        for (int l = 0; l < G; ++l) {
+            Work& w = m->lane[l];
+            const int rows = g0[l + 1] - g0[l];
+            if (rows > w.rows) { g_prof = nullptr; return set_error(LBC_E_STATE, "decoder lane workspace too small"); }
+            RansArgs r{};
+            r.cdf16 = m->cdf16_dev.as<uint16_t>();
+            r.tmeta = m->tmeta_dev.as<int>();
+            r.table = m->table_dev.as<float>();
+            r.total16 = m->total16;
+            r.words = m->words.as<uint32_t>();
+            r.word_base = m->word_base.as<long long>();
+            r.word_count = m->word_count.as<int>();
+            r.state_x = m->st_x.as<unsigned long long>();
+            r.state_ptr = m->st_ptr.as<int>();
+            r.status = m->st_status.as<int>();
+            r.idx = w.idx.as<int32_t>();
+            r.ksi = w.ksi.as<float>();
+            r.ldk = m->C4;
+            r.Mlat = m->M;
+            r.yq = w.yq.as<float>();
+            r.ldy = m->M;
+            r.rows = rows;
+            r.ctr = m->ctr.as<int>() + l;
+            r.ctr_stride = Wb * n_img;
+            HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
+            int crc = prof_range_begin(&m->prof, 1 + l, m->cap);
+            drop_recs(m->prof, 1 + l);
+            for (int h = 0; h < Wb && !crc; ++h) {
+                m->prof.active = m->prof.sample_every > 0 && (h % m->prof.sample_every) == 0;
+                const int4* blocks = m->blocks_dec.as<int4>() + (size_t)h * n_img + g0[l];
+                GemmArgs g = base_args(m, blocks, rows, nullptr, n_img, Hb, Wb);
+                g.ctr = r.ctr;
+                g.ctr_stride = r.ctr_stride;
+                if (!crc) crc = run_ctx(m, w, g, true, m->cap);
+                r.blocks = blocks;
+                r.ts = m->prof.active ? m->prof.take() : nullptr;
+                if (!crc) crc = launch_rans_decode(r, m->cap);
+                if (!crc && r.ts) {
+                    // algorithmic bytes: the CDF tables staged into LDS + idx/mean in + y_qnt out
+                    const double b = (double)m->total16 * 2 * ((rows + 7) / 8) + 12.0 * rows * m->M;
+                    m->prof.recs.push_back({2, (int)((r.ts - m->prof.slots) / kSlotU64), 0.0, b});
+                }
+                if (!crc) crc = run_dec(m, w, g, m->cap);
+            }
+            if (!crc) crc = launch_ctr_add(m->ctr.as<int>() + l, 1, m->cap);
+            hipGraph_t graph = nullptr;
+            const hipError_t e = hipStreamEndCapture(m->cap, &graph);
+            if (crc) { if (graph) (void)hipGraphDestroy(graph); g_prof = nullptr; return crc; }
+            if (e != hipSuccess) return set_error(LBC_E_HIP, std::string("decoder capture: ") + hipGetErrorString(e));
+            hipGraphExec_t ex = nullptr;
+            const hipError_t ei = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            if (ei != hipSuccess) return set_error(LBC_E_HIP, std::string("decoder instantiate: ") + hipGetErrorString(ei));
+            m->dec_exec.push_back(ex);
         }
-        if ((rc = run_dec(m, g, s))) return rc;
+        m->prof.active = false;
+        g_prof = nullptr;
+        m->dec_key = key;
+    }
+    HIPCHK(hipMemsetAsync(m->ctr.p, 0, kLanes * sizeof(int), s));
+    HIPCHK(hipEventRecord(m->lev[kLanes], s));
+    for (int l = 0; l < G; ++l) HIPCHK(hipStreamWaitEvent(m->lstream[l], m->lev[kLanes], 0));
+    for (int v = 0; v < Hb; ++v)
+        for (int l = 0; l < G; ++l) HIPCHK(hipGraphLaunch(m->dec_exec[l], m->lstream[l]));
+    for (int l = 0; l < G; ++l) {
+        HIPCHK(hipEventRecord(m->lev[l], m->lstream[l]));
+        HIPCHK(hipStreamWaitEvent(s, m->lev[l], 0));
     }
     m->prof.active = false;
     g_prof = nullptr;
@@ -715,34 +849,53 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
 
 int lbc_profile_begin(lbc_model* m, int sample_every) {
     if (!m || sample_every < 0) return set_error(LBC_E_ARG, "bad argument");
-    m->prof.sample_every = sample_every;
-    m->prof.recs.clear();
-    m->prof.used = 0;
+    Prof& p = m->prof;
+    if (sample_every && !p.slots) {
+        HIPCHK(hipSetDevice(m->cfg.device));
+        HIPCHK(hipMalloc(&p.slots, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
+        HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
+    }
+    p.sample_every = sample_every;   // part of the graph keys: the next encode / decode re-captures
+    p.recs.clear();
     return LBC_OK;
 }
 
+// Reads the stamps of the sampled launches as of the last replay of every graph (a decoder row graph
+// is replayed Hb times: its stamps are those of the last block row).
 int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out) {
     if (!m || !out || !n_out) return set_error(LBC_E_ARG, "null argument");
     Prof& p = m->prof;
     lbc_kernel_stat acc[4];
     std::memset(acc, 0, sizeof(acc));
     for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", kKernelNames[c]);
-    if (!p.recs.empty()) HIPCHK(hipEventSynchronize(p.pool[p.used - 1]));
-    for (const auto& r : p.recs) {
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, p.pool[r.ev], p.pool[r.ev + 1]));
-        acc[r.cls].launches += 1;
-        acc[r.cls].total_ms += ms;
-        acc[r.cls].flops += r.flops;
-        acc[r.cls].bytes += r.bytes;
+    if (p.slots && !p.recs.empty()) {
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1));
+        HIPCHK(hipMemcpy(h.data(), p.slots, h.size() * 8, hipMemcpyDeviceToHost));
+        for (const auto& r : p.recs) {
+            const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;
+            long long span = -1;
+            for (int x = 0; x < 8; ++x) {
+                if (!t[2 * x] || !t[2 * x + 1]) continue;
+                const long long d = (long long)(t[2 * x + 1] - (~0ull - t[2 * x]));
+                if (d >= 0 && d > span) span = d;
+            }
+            if (getenv("LBIC_DEBUG_STAMPS") && span > 10000000) {
+                fprintf(stderr, "bad slot %d cls %d:", r.slot, r.cls);
+                for (int x = 0; x < 16; ++x) fprintf(stderr, " %llx", t[x]);
+                fprintf(stderr, "\n");
+            }
+            if (span < 0) continue;   // not executed since the last reset
+            acc[r.cls].launches += 1;
+            acc[r.cls].total_ms += (double)span * 1e-5;     // 100 MHz ticks -> ms
+            acc[r.cls].flops += r.flops;
+            acc[r.cls].bytes += r.bytes;
+        }
     }
     int n = 0;
     for (int c = 0; c < 4 && n < max_out; ++c)
         if (acc[c].launches) out[n++] = acc[c];
     *n_out = n;
-    p.sample_every = 0;
-    p.recs.clear();
-    p.used = 0;
     return LBC_OK;
 }
 

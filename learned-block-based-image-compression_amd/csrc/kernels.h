@@ -42,10 +42,14 @@ struct GemmArgs {
     Seg seg[6];
     int pos_dy[5], pos_dx[5];
     const int4* blocks;      // per block (img, v, h, 0); row r belongs to block r / P
+    const int* ctr;          // optional device counter: blocks += *ctr * ctr_stride (graph replays per row)
+    int ctr_stride;
+    unsigned long long* ts;  // optional timing slot {max(~start), max(end)} in s_memrealtime ticks (100 MHz)
     const float* W;
     int NB16;                // N padded / 16
     const float* bias;       // bias (beta for GDN)
     int epi, square_a;
+    int need_blocks;         // set by launch_gemm: a z-tap / x segment or a scattering epilogue
     float* out;
     int ldo;
     const float* gx;         // GDN: the layer input x (epilogue x * rsqrt(norm))
@@ -63,6 +67,7 @@ struct GemmArgs {
 struct RansArgs {
     const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit)
     const int* tmeta;        // [3][64]: base, cdf_length, offset
+    const float* table;      // scale table (64): the Gaussian sigma of each CDF
     int total16;             // entries in cdf16 (even)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;
@@ -76,11 +81,15 @@ struct RansArgs {
     float* yq;
     int ldy;
     const int4* blocks;
+    const int* ctr;
+    int ctr_stride;
+    unsigned long long* ts;
     int rows;
 };
 
-int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = <32,16,8>, 1 = <64,32,4>
+int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = <16,16,8>, 1 = <64,32,4>
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
+int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
 
 }  // namespace lbic

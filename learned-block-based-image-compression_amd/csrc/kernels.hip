@@ -25,6 +25,40 @@ namespace lbic {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// Launch-span stamps for sampled launches (bench.py's per-kernel roofline).  HIP events cannot be
+// recorded inside a captured graph on ROCm 7.2, so the kernels stamp themselves on the constant 100 MHz
+// clock: per XCD (the counters of different XCDs need not agree) the earliest workgroup start and the
+// latest workgroup end, slot = 8 x {max(~start), max(end)}; slots are zeroed at every graph replay.
+__device__ __forceinline__ int xcc_id() {
+    int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 7;
+}
+__device__ __forceinline__ void stamp_start(unsigned long long* ts) {
+    if (ts && threadIdx.x == 0)
+        atomicMax(ts + 2 * xcc_id(), ~0ull - (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long* ts) {
+    if (ts) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            atomicMax(ts + 2 * xcc_id() + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+    }
+}
+
+#ifdef LBIC_PHASE_STAMPS
+// diagnostic build only (csrc/microbench.hip): per-workgroup s_memtime at phase boundaries
+__device__ unsigned long long* g_phase;
+#define PHASE(i)                                                                                  \
+    do {                                                                                          \
+        if (threadIdx.x == 0) g_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PHASE(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ int scale_index(float s, const float* table) {
     // build_indexes (entropy_layers_cai.py:649-654): idx = 63 - #{k < 63 : max(s, .11) <= table[k]}
     s = fmaxf(s, 0.11f);
@@ -39,26 +73,94 @@ __device__ __forceinline__ float std_cum(float x) {
     return 0.5f * erfcf(-0.70710677f * x);
 }
 
-template <int BM, int BN, int NW>
+// A / W fragments of one 16-wide k-block for this lane (operand maps: the packing comment in codec.hip)
+template <int MS, int NS>
+struct Frag {
+    f4 a[MS];
+    f4 w[NS];
+};
+
+constexpr int MAXSEG = 6;
+
+// Source addressing without branches in the k-loop: every lane precomputes, per segment t and row
+// subtile s, a 32-bit element offset from that segment's base pointer; a k-block then selects its
+// segment with uniform compares (SALU) and the offset with v_cndmask, so the compiler never branches
+// around a load (a branch per load makes hipcc drain vmcnt(0) each time: cdna_hip_programming.md §5,
+// "Three .s-level traps", (c)).
+template <int MS>
+struct Rows {
+    int off[MAXSEG][MS];
+};
+
+template <int MS, int NS>
+__device__ __forceinline__ void load_kb(const GemmArgs& g, int kb, int nb0, const Rows<MS>& R, int q4, int lane,
+                                        Frag<MS, NS>& f) {
+    const int k = kb << 4;
+    const float* base = g.seg[0].base;
+    int k0 = g.seg[0].k0;
+    int o[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) o[s] = R.off[0][s];
+#pragma unroll
+    for (int t = 1; t < MAXSEG; ++t) {
+        const bool in = t < g.nseg && k >= g.seg[t].k0;     // wave-uniform
+        base = in ? g.seg[t].base : base;
+        k0 = in ? g.seg[t].k0 : k0;
+#pragma unroll
+        for (int s = 0; s < MS; ++s) o[s] = in ? R.off[t][s] : o[s];
+    }
+    const int kk = k - k0 + q4;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) f.a[s] = *reinterpret_cast<const f4*>(base + o[s] + kk);
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) f.w[j] = Wt[((long)kb * g.NB16 + nb0 + j) * 64];
+}
+
+template <int MS, int NS>
+__device__ __forceinline__ void mma_kb(const GemmArgs& g, Frag<MS, NS>& f, f4 (&acc)[MS][NS]) {
+    if (g.square_a) {
+#pragma unroll
+        for (int s = 0; s < MS; ++s) f.a[s] = f.a[s] * f.a[s];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+#pragma unroll
+            for (int j = 0; j < NS; ++j)
+                acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[s][e], f.w[j][e], acc[s][j], 0, 0, 0);
+}
+
+// CH k-blocks per chunk: all their loads are issued together, and chunk c+1 is in flight while chunk c
+// is multiplied, so a slice of K costs about one memory round trip instead of one per k-block.
+template <int BM, int BN, int NW, int CH>
 __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
     constexpr int MS = BM / 16, NS = BN / 16, SPW = KSPLIT / NW;
     extern __shared__ __attribute__((aligned(16))) float red[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: keeps the k-loop scalar
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
     const int q4 = (lane >> 4) * 4;
 
-    // per-lane source offsets of the rows this lane feeds (row = lane&15 of each 16-row subtile)
-    long zoff[MS], xoff[MS];
-    int drow[MS];
+    stamp_start(g.ts);
+    PHASE(0);
+    const int4* blocks = g.ctr ? g.blocks + (long)(*g.ctr) * g.ctr_stride : g.blocks;
+    // per-lane, per-segment element offsets of the rows this lane feeds (row = lane&15 of each subtile)
+    Rows<MS> R;
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
         const int r = min(m0 + 16 * s + (lane & 15), g.M - 1);
-        drow[s] = r;
         const int m = r / g.P, p = r - m * g.P;
-        const int4 b = g.blocks[m];
-        const int vv = b.y + 2 + g.pos_dy[p], hh = b.z + 2 + g.pos_dx[p];
-        zoff[s] = ((long)(b.x * g.geo.Hp + vv) * g.geo.Wp + hh) * g.geo.Cx;
-        xoff[s] = ((long)(b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
+        const int4 b = g.need_blocks ? blocks[m] : make_int4(0, 0, 0, 0);   // dense-only GEMMs skip this load
+        const int zrow = ((b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p]) * g.geo.Cx;
+        const int xrow = ((b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
+#pragma unroll
+        for (int t = 0; t < MAXSEG; ++t) {
+            const Seg& sg = g.seg[t < g.nseg ? t : 0];
+            R.off[t][s] = sg.kind == SEG_DENSE ? r * sg.ld
+                        : sg.kind == SEG_ZTAP ? zrow + (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : xrow;
+        }
     }
 
     f4 acc[SPW][MS][NS];
@@ -68,43 +170,41 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         for (int s = 0; s < MS; ++s)
 #pragma unroll
             for (int j = 0; j < NS; ++j) acc[q][s][j] = f4{0.f, 0.f, 0.f, 0.f};
+    PHASE(1);
 
     const int nkb = g.K >> 4;
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     const int nb0 = n0 >> 4;
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
         const int slice = wave + q * NW;
         const int kb0 = slice * nkb / KSPLIT, kb1 = (slice + 1) * nkb / KSPLIT;
-        int si = 0;
-        for (int kb = kb0; kb < kb1; ++kb) {
-            const int k = kb << 4;
-            while (k >= g.seg[si].k1) ++si;     // wave-uniform
-            const Seg& sg = g.seg[si];
-            const int kk = k - sg.k0 + q4;
-            f4 a[MS];
+        if (kb0 >= kb1) continue;
+        Frag<MS, NS> fa[CH], fb[CH];
+        // out-of-range k-blocks of the last chunk re-load the slice's last block (valid address) and
+        // skip their MFMAs, so the summation order is the plain k order for every CH
+        auto load_chunk = [&](int base, Frag<MS, NS>(&f)[CH]) {
 #pragma unroll
-            for (int s = 0; s < MS; ++s) {
-                const float* src;
-                if (sg.kind == SEG_DENSE) src = sg.base + (long)drow[s] * sg.ld;
-                else if (sg.kind == SEG_ZTAP) src = g.geo.zpad + zoff[s] + (long)(sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx;
-                else src = g.geo.x + xoff[s];
-                a[s] = *reinterpret_cast<const f4*>(src + kk);
-                if (g.square_a) a[s] = a[s] * a[s];
-            }
-            f4 w[NS];
+            for (int c = 0; c < CH; ++c) load_kb<MS, NS>(g, min(base + c, kb1 - 1), nb0, R, q4, lane, f[c]);
+        };
+        auto mma_chunk = [&](int base, Frag<MS, NS>(&f)[CH]) {
 #pragma unroll
-            for (int j = 0; j < NS; ++j) w[j] = Wt[((long)kb * g.NB16 + nb0 + j) * 64];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int s = 0; s < MS; ++s)
-#pragma unroll
-                    for (int j = 0; j < NS; ++j)
-                        acc[q][s][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][e], w[j][e], acc[q][s][j], 0, 0, 0);
+            for (int c = 0; c < CH; ++c)
+                if (base + c < kb1) mma_kb<MS, NS>(g, f[c], acc[q]);
+        };
+        int kb = kb0;
+        load_chunk(kb, fa);
+        while (kb < kb1) {               // two named buffers, statically indexed (no scratch)
+            if (kb + CH < kb1) load_chunk(kb + CH, fb);
+            mma_chunk(kb, fa);
+            kb += CH;
+            if (kb >= kb1) break;
+            if (kb + CH < kb1) load_chunk(kb + CH, fa);
+            mma_chunk(kb, fb);
+            kb += CH;
         }
     }
 
+    PHASE(2);
     // partials -> LDS [slice][((s*NS + j)*4 + r)*64 + lane]
     constexpr int TE = BM * BN;
 #pragma unroll
@@ -118,6 +218,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
                 for (int r = 0; r < 4; ++r) dst[((s * NS + j) * 4 + r) * 64 + lane] = acc[q][s][j][r];
     }
     __syncthreads();
+    PHASE(3);
 
     for (int e = threadIdx.x; e < TE; e += NW * 64) {
         float v = red[e];
@@ -152,7 +253,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
                 const int sym = (int)rintf(d);               // torch.round: half to even
                 const float yq = (float)sym + mean;
                 g.out[(long)row * g.ldo + col] = yq;
-                const int4 b = g.blocks[row];
+                const int4 b = blocks[row];
                 const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
                 g.sym[pos] = sym;
                 g.idx[pos] = scale_index(scale, g.table);
@@ -171,66 +272,89 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
             }
             case EPI_CLAMPZ: {
                 const float t = fminf(fmaxf(v + g.bias[col], -0.5f), 0.5f);
-                const int4 b = g.blocks[row];
+                const int4 b = blocks[row];
                 g.geo.zpad[((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col] = t;
                 break;
             }
         }
     }
+    PHASE(4);
+    stamp_end(g.ts);
 }
 
-template <int BM, int BN, int NW>
+template <int BM, int BN, int NW, int CH>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = (size_t)KSPLIT * BM * BN * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW>), grid, dim3(NW * 64), lds, s, g);
+    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH>), grid, dim3(NW * 64), lds, s, g);
     return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm launch failed");
 }
 
-int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id) {
+int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
+    GemmArgs g = g0;
+    g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ;
+    for (int t = 0; t < g.nseg && t < MAXSEG; ++t) g.need_blocks |= g.seg[t].kind != SEG_DENSE;
     if (g.M <= 0) return LBC_OK;
     if (g.K % 16 || g.K < 16) return set_error(LBC_E_ARG, "GEMM K must be a positive multiple of 16");
-    if (g.M <= 64) {
+    // host-side checks of what the kernel assumes: contiguous 16-aligned segments with real bases
+    if (g.nseg < 1 || g.nseg > MAXSEG || g.seg[0].k0 != 0 || g.seg[g.nseg - 1].k1 < g.K)
+        return set_error(LBC_E_ARG, "GEMM segments must cover [0, K)");
+    for (int t = 0; t < g.nseg; ++t) {
+        const Seg& sg = g.seg[t];
+        if (!sg.base || (sg.k0 & 15) || (t && sg.k0 != g.seg[t - 1].k1))
+            return set_error(LBC_E_ARG, "bad GEMM segment");
+    }
+    if (!g.W || !g.bias || !g.blocks || g.P < 1 || g.P > 5) return set_error(LBC_E_ARG, "bad GEMM arguments");
+    if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): more, lighter tiles
         if (cfg_id) *cfg_id = 0;
-        return launch_cfg<32, 16, 8>(g, s);
+        return launch_cfg<16, 16, 8, 4>(g, s);
     }
     if (cfg_id) *cfg_id = 1;
-    return launch_cfg<64, 32, 4>(g, s);
+    return launch_cfg<64, 32, 4, 2>(g, s);
 }
 
 // ----------------------------------------------------------------------------------------- rANS decode
 // One 64-lane wave per image decodes that image's Mlat symbols of the current block (RansDecoder::
-// decode_stream, called per block at net:439), entirely on the GPU: the CDF tables live in LDS as
-// 16-bit entries, each symbol's search is one wave-wide window compare (ballot + popcount) around the
-// table centre, the 64-bit state stays wave-uniform.  Output: y_qnt = sym + mean (dequantize,
-// entropy_layers_cai.py:159-168, net:440-442) for the decoder's first layer.
-__global__ __launch_bounds__(64) void k_rans_decode(const RansArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
-    const int lane = threadIdx.x;
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cdf16);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(lcdf);
-        for (int i = lane; i < a.total16 / 2; i += 64) dst[i] = src[i];
-    }
-    __syncthreads();
-    const int row = blockIdx.x;
-    const int img = a.blocks[row].x;
+// decode_stream, called per block at net:439), entirely on the GPU.  Up to 8 images share a workgroup
+// and one LDS copy of the 16-bit CDF tables.  Per symbol: one wave-wide window compare (ballot +
+// popcount) around the table centre gives the symbol, v_readlane pulls its CDF interval out of the
+// window, and the next 64 stream words sit lane-distributed in a register (renormalisation is a
+// readlane, not a dependent global load).  The 64-bit state is wave-uniform.  Output:
+// y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
+constexpr int RANS_WPB = 8;      // waves (images) per workgroup
+constexpr int RANS_MAXLAT = 256; // Mlat <= 4 * 64
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+__device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, int row, int lane) {
+    const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
+    const int img = __builtin_amdgcn_readfirstlane(blocks[row].x);
+    const int Mlat = a.Mlat;
+    // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
+    const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
+    const float t_sig = a.table[lane];
     unsigned long long x = a.state_x[img];
     int p = a.state_ptr[img];
     const uint32_t* w = a.words + a.word_base[img];
     const int nw = a.word_count[img];
+    int p0 = p;
+    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
     int bad = 0;
     auto next_word = [&]() -> uint32_t {
-        uint32_t v = 0;
-        if (p < nw) v = w[p]; else bad = 1;
+        if (p - p0 >= 64) {
+            p0 = p;
+            wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+        }
+        if (p >= nw) bad = 1;
+        const uint32_t v = rdlane(wbuf, p - p0);
         ++p;
-        return v;
+        return p - 1 < nw ? v : 0u;
     };
     auto get_bits = [&](int nb) -> uint32_t {
         const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
@@ -238,41 +362,60 @@ __global__ __launch_bounds__(64) void k_rans_decode(const RansArgs a) {
         if (x < (1ull << 31)) x = (x << 32) | next_word();
         return v;
     };
-    for (int i = 0; i < a.Mlat; ++i) {
-        const int ci = a.idx[(long)row * a.Mlat + i];
-        if (ci < 0 || ci > 63) { bad = 2; break; }
-        const int base = a.tmeta[ci], len = a.tmeta[64 + ci], off = a.tmeta[128 + ci];
-        const uint32_t cum = (uint32_t)(x & 0xffff);
-        int lo = max(0, -off - 31);
-        int s;
-        for (;;) {
-            const int j = lo + lane;
-            const uint32_t c = j < len - 1 ? (uint32_t)lcdf[base + j] : 65536u;
-            const unsigned long long m = __ballot(c <= cum);
-            const int cnt = __popcll(m);
-            if (cnt == 0) { lo = max(0, lo - 63); continue; }
-            if (cnt == 64) { lo += 63; continue; }
-            s = lo + cnt - 1;
-            break;
+    int idxr[4], symr[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int i = kb * 64 + lane;
+        idxr[kb] = i < Mlat ? a.idx[(long)row * Mlat + i] : 0;
+        symr[kb] = 0;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int cnt_i = min(64, Mlat - kb * 64);
+        for (int ii = 0; ii < cnt_i && !bad; ++ii) {
+            const int ci = __builtin_amdgcn_readlane(idxr[kb], ii);
+            if (ci < 0 || ci > 63) { bad = 2; break; }
+            const int base = __builtin_amdgcn_readlane(t_base, ci);
+            const int len = __builtin_amdgcn_readlane(t_len, ci);
+            const int off = __builtin_amdgcn_readlane(t_off, ci);
+            const uint32_t cum = (uint32_t)(x & 0xffff);
+            // start the window at the Gaussian quantile of cum (the table is the quantised CDF of
+            // N(0, sigma) centred at -off): one window read finds the symbol almost always
+            const float sig = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t_sig), ci));
+            const float z = 1.41421356f * erfinvf(fminf(fmaxf(((float)cum + 0.5f) * (2.0f / 65536.0f) - 1.0f, -0.999999f), 0.999999f));
+            int guess = -off + (int)rintf(sig * z);
+            int lo = min(max(0, guess - 31), max(0, len - 64));
+            uint32_t c;
+            int cnt;
+            for (;;) {
+                const int j = lo + lane;
+                c = j < len - 1 ? (uint32_t)lcdf[base + j] : 65536u;
+                cnt = __popcll(__ballot(c <= cum));
+                if (cnt == 0) { lo = max(0, lo - 63); continue; }
+                if (cnt == 64) { lo += 63; continue; }
+                break;
+            }
+            const int sidx = lo + cnt - 1;
+            const uint32_t start = rdlane(c, cnt - 1), nxt = rdlane(c, cnt);
+            x = (unsigned long long)(nxt - start) * (x >> 16) + (x & 0xffff) - start;
+            if (x < (1ull << 31)) x = (x << 32) | next_word();
+            int v = sidx;
+            if (v == len - 2) {   // escape: value coded in 4-bit bypass chunks
+                uint32_t cc = get_bits(4), nb = cc;
+                while (cc == 15u && nb <= 8) { cc = get_bits(4); nb += cc; }
+                if (nb > 8) { bad = 3; break; }
+                uint32_t raw = 0;
+                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits(4) << (jj * 4);
+                v = (int)(raw >> 1);
+                v = (raw & 1) ? -v - 1 : v + len - 2;
+            }
+            if (lane == ii) symr[kb] = v + off;
         }
-        const uint32_t start = lcdf[base + s];
-        const uint32_t nxt = (s + 1 >= len - 1) ? 65536u : (uint32_t)lcdf[base + s + 1];
-        x = (unsigned long long)(nxt - start) * (x >> 16) + (x & 0xffff) - start;
-        if (x < (1ull << 31)) x = (x << 32) | next_word();
-        int v = s;
-        if (v == len - 2) {   // escape: value coded in 4-bit bypass chunks
-            uint32_t c = get_bits(4), nb = c;
-            while (c == 15u) { c = get_bits(4); nb += c; }
-            if (nb > 8) { bad = 3; break; }
-            uint32_t raw = 0;
-            for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits(4) << (jj * 4);
-            v = (int)(raw >> 1);
-            v = (raw & 1) ? -v - 1 : v + len - 2;
-        }
-        if (lane == 0) {
-            const float mean = a.ksi[(long)row * a.ldk + a.Mlat + i];
-            a.yq[(long)row * a.ldy + i] = (float)(v + off) + mean;
-        }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int i = kb * 64 + lane;
+        if (i < Mlat) a.yq[(long)row * a.ldy + i] = (float)symr[kb] + a.ksi[(long)row * a.ldk + Mlat + i];
     }
     if (lane == 0) {
         a.state_x[img] = x;
@@ -281,16 +424,41 @@ __global__ __launch_bounds__(64) void k_rans_decode(const RansArgs a) {
     }
 }
 
+__global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
+    stamp_start(a.ts);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
+        uint4* dst = reinterpret_cast<uint4*>(lcdf);
+        for (int i = threadIdx.x; i < a.total16 / 8; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * RANS_WPB + (threadIdx.x >> 6);
+    if (row < a.rows) rans_row(a, lcdf, row, lane);
+    stamp_end(a.ts);
+}
+
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
+    if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
+    if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 table must be padded to 16 bytes");
     const size_t lds = (size_t)a.total16 * sizeof(uint16_t);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_rans_decode, dim3(a.rows), dim3(64), lds, s, a);
+    const int wpb = a.rows < RANS_WPB ? a.rows : RANS_WPB;
+    hipLaunchKernelGGL(k_rans_decode, dim3((a.rows + RANS_WPB - 1) / RANS_WPB), dim3(wpb * 64), lds, s, a);
     return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_rans_decode launch failed");
+}
+
+__global__ void k_ctr_add(int* c, int d) { *c += d; }
+
+int launch_ctr_add(int* ctr, int d, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, s, ctr, d);
+    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "ctr launch failed");
 }
 
 __global__ void k_copy_interior(const float* __restrict__ zpad, float* __restrict__ zout, int n_img, int Hb, int Wb,
