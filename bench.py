@@ -147,6 +147,7 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    model.profile_begin(args.sample_every)     # same period: keeps the graphs, restarts launch counts
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -193,9 +194,11 @@ def main():
     if kstats:
         for name, s in kstats.items():
             avg = s["total_ms"] / max(s["launches"], 1)
-            kernels[name] = dict(launches_sampled=s["launches"], avg_us=round(avg * 1e3, 3),
-                                 total_ms_sampled=round(s["total_ms"], 3))
-        dom = max(kstats, key=lambda k: kstats[k]["total_ms"])
+            kernels[name] = dict(launches_sampled=s["launches"], launches_total=s["total_launches"],
+                                 avg_us=round(avg * 1e3, 3),
+                                 est_share_of_step=round(avg * s["total_launches"] / 1e3 / dt, 4))
+        # dominant kernel: sampled average duration x true launch count over the timed region
+        dom = max(kstats, key=lambda k: kstats[k]["total_ms"] / max(kstats[k]["launches"], 1) * kstats[k]["total_launches"])
         s = kstats[dom]
         t_s = s["total_ms"] / 1e3
         ai = s["flops"] / s["bytes"] if s["bytes"] else float("inf")

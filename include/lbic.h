@@ -106,6 +106,7 @@ int lbc_last_timing(const lbc_model *m, double *enc_ms, double *dec_ms);
 typedef struct {
     char name[40];
     long long launches;   /* sampled launches */
+    long long total_launches; /* all launches of this kernel since lbc_profile_begin */
     double total_ms;      /* summed event-to-event durations */
     double flops;         /* summed algorithmic FLOPs (2 * rows * K_live * N for a GEMM) */
     double bytes;         /* summed algorithmic bytes (weights + A rows + outputs read/written once) */

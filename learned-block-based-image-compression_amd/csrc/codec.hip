@@ -76,6 +76,8 @@ struct Prof {
     std::vector<Rec> recs;
     unsigned long long* slots = nullptr;   // device, kLanes + 1 ranges
     int range = 0, next = 0;               // slot allocation inside the range being captured
+    long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
+    long long replays[8] = {};             // replays of each range's graph since lbc_profile_begin
     unsigned long long* take() {
         if (!slots || next >= kSlotsPerRange) return nullptr;
         return slots + kSlotU64 * ((size_t)range * kSlotsPerRange + next++);
@@ -328,6 +330,7 @@ void drop_recs(Prof& p, int r) {
 int prof_range_begin(Prof* p, int r, hipStream_t s) {
     p->range = r;
     p->next = 0;
+    for (auto& c : p->per_replay[r]) c = 0;
     if (p->sample_every && p->slots)
         HIPCHK(hipMemsetAsync(p->slots + kSlotU64 * (size_t)r * kSlotsPerRange, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange, s));
     return LBC_OK;
@@ -336,6 +339,7 @@ int prof_range_begin(Prof* p, int r, hipStream_t s) {
 // launch a GEMM; in a sampled step give it a timing slot and record its algorithmic work
 int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     Prof* p = g_prof;
+    if (p) p->per_replay[p->range][g0.M <= 64 ? 0 : 1] += 1;   // the class launch_gemm will pick
     if (!p || !p->active) return launch_gemm(g0, s);
     GemmArgs g = g0;
     g.ts = p->take();
@@ -626,8 +630,13 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
         c16.push_back(0);   // slot of the implicit final 2^16
     }
     while (c16.size() & 7) c16.push_back(0);   // 16-byte granules for the LDS staging loads
+    {   // the decoder's start-index LUT follows the tables (k_rans_decode stages both into LDS)
+        std::vector<uint16_t> lut;
+        build_start_lut(t, lut);
+        m->total16 = (int)c16.size();
+        c16.insert(c16.end(), lut.begin(), lut.end());
+    }
     if (c16.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
-    m->total16 = (int)c16.size();
     m->c16_host = std::move(c16);
     m->meta_host = std::move(meta);
     m->tabs_set = true;
@@ -685,6 +694,7 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
     HIPCHK(hipMemcpyAsync(m->x_in.p, x_dev, nx * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
     HIPCHK(hipGraphLaunch(m->enc_exec, s));
+    m->prof.replays[0] += 1;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipMemcpyAsync(sym_dev, m->sym_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(idx_dev, m->idx_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
@@ -773,7 +783,6 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             RansArgs r{};
             r.cdf16 = m->cdf16_dev.as<uint16_t>();
             r.tmeta = m->tmeta_dev.as<int>();
-            r.table = m->table_dev.as<float>();
             r.total16 = m->total16;
             r.words = m->words.as<uint32_t>();
             r.word_base = m->word_base.as<long long>();
@@ -802,6 +811,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
                 if (!crc) crc = run_ctx(m, w, g, true, m->cap);
                 r.blocks = blocks;
                 r.ts = m->prof.active ? m->prof.take() : nullptr;
+                m->prof.per_replay[1 + l][2] += 1;
                 if (!crc) crc = launch_rans_decode(r, m->cap);
                 if (!crc && r.ts) {
                     // algorithmic bytes: the CDF tables staged into LDS + idx/mean in + y_qnt out
@@ -830,6 +840,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     for (int l = 0; l < G; ++l) HIPCHK(hipStreamWaitEvent(m->lstream[l], m->lev[kLanes], 0));
     for (int v = 0; v < Hb; ++v)
         for (int l = 0; l < G; ++l) HIPCHK(hipGraphLaunch(m->dec_exec[l], m->lstream[l]));
+    for (int l = 0; l < G; ++l) m->prof.replays[1 + l] += Hb;
     for (int l = 0; l < G; ++l) {
         HIPCHK(hipEventRecord(m->lev[l], m->lstream[l]));
         HIPCHK(hipStreamWaitEvent(s, m->lev[l], 0));
@@ -855,8 +866,11 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
         HIPCHK(hipMalloc(&p.slots, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
         HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
     }
-    p.sample_every = sample_every;   // part of the graph keys: the next encode / decode re-captures
-    p.recs.clear();
+    // sample_every is part of the graph keys: a change re-captures (and re-creates the sample records);
+    // an unchanged value only restarts the launch counting
+    if (sample_every != p.sample_every) p.recs.clear();
+    p.sample_every = sample_every;
+    for (auto& r : p.replays) r = 0;
     return LBC_OK;
 }
 
@@ -891,6 +905,12 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
             acc[r.cls].flops += r.flops;
             acc[r.cls].bytes += r.bytes;
         }
+    }
+    // true launch counts since lbc_profile_begin (the stamps are a sample of them)
+    for (int c = 0; c < 4; ++c) {
+        long long tot = 0;
+        for (int r = 0; r < 8; ++r) tot += p.per_replay[r][c] * p.replays[r];
+        acc[c].total_launches = tot;
     }
     int n = 0;
     for (int c = 0; c < 4 && n < max_out; ++c)

@@ -149,4 +149,19 @@ int rans_decode_host(const EntropyTables& t, const uint8_t* data, size_t len, co
     return LBC_OK;
 }
 
+// For the GPU decoder: per table, the symbol index whose interval contains cum = 256*q (q = 0..255),
+// i.e. the largest s with cdf[s] <= 256*q.  A symbol with cum in bucket q lies in [lut[q], lut[q+1]].
+void build_start_lut(const EntropyTables& t, std::vector<uint16_t>& lut) {
+    lut.assign((size_t)t.n_tables * 256, 0);
+    for (int i = 0; i < t.n_tables; ++i) {
+        const int32_t* cdf = t.cdf.data() + (size_t)i * t.stride;
+        int s = 0;
+        for (int q = 0; q < 256; ++q) {
+            const int32_t c = 256 * q;
+            while (s + 1 <= t.length[i] - 2 && cdf[s + 1] <= c) ++s;
+            lut[(size_t)i * 256 + q] = (uint16_t)s;
+        }
+    }
+}
+
 }  // namespace lbic

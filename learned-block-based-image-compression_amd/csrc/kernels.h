@@ -65,9 +65,9 @@ struct GemmArgs {
 };
 
 struct RansArgs {
-    const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit)
+    const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit),
+                             // then the 64 x 256 start-index LUT (build_start_lut)
     const int* tmeta;        // [3][64]: base, cdf_length, offset
-    const float* table;      // scale table (64): the Gaussian sigma of each CDF
     int total16;             // entries in cdf16 (even)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;

@@ -41,10 +41,7 @@ __device__ __forceinline__ void stamp_start(unsigned long long* ts) {
 __device__ __forceinline__ void stamp_end(unsigned long long* ts) {
     if (ts) {
         __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            atomicMax(ts + 2 * xcc_id() + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
+        if (threadIdx.x == 0) atomicMax(ts + 2 * xcc_id() + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }
 
@@ -54,6 +51,7 @@ __device__ unsigned long long* g_phase;
 #define PHASE(i)                                                                                  \
     do {                                                                                          \
         if (threadIdx.x == 0) g_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0 && (i) == 0) g_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + 7] = xcc_id(); \
     } while (0)
 #else
 #define PHASE(i) do {} while (0)
@@ -332,36 +330,24 @@ constexpr int RANS_MAXLAT = 256; // Mlat <= 4 * 64
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
-__device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, int row, int lane) {
+__device__ __forceinline__ unsigned long long uni64(unsigned long long v) {   // keep a uniform value in SGPRs
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
+                                         int lane) {
     const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
     const int img = __builtin_amdgcn_readfirstlane(blocks[row].x);
     const int Mlat = a.Mlat;
     // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
     const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
-    const float t_sig = a.table[lane];
-    unsigned long long x = a.state_x[img];
-    int p = a.state_ptr[img];
+    unsigned long long x = uni64(a.state_x[img]);
+    int p = __builtin_amdgcn_readfirstlane(a.state_ptr[img]);
     const uint32_t* w = a.words + a.word_base[img];
-    const int nw = a.word_count[img];
+    const int nw = __builtin_amdgcn_readfirstlane(a.word_count[img]);
     int p0 = p;
     uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-    int bad = 0;
-    auto next_word = [&]() -> uint32_t {
-        if (p - p0 >= 64) {
-            p0 = p;
-            wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-        }
-        if (p >= nw) bad = 1;
-        const uint32_t v = rdlane(wbuf, p - p0);
-        ++p;
-        return p - 1 < nw ? v : 0u;
-    };
-    auto get_bits = [&](int nb) -> uint32_t {
-        const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
-        x >>= nb;
-        if (x < (1ull << 31)) x = (x << 32) | next_word();
-        return v;
-    };
     int idxr[4], symr[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -369,41 +355,59 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
         idxr[kb] = i < Mlat ? a.idx[(long)row * Mlat + i] : 0;
         symr[kb] = 0;
     }
+    int bad = 0;
+    // next stream word (lane-distributed window of 64 words; reloaded every 64 words)
+    auto next_word = [&]() -> uint32_t {
+        if (p - p0 >= 64) {
+            p0 = p;
+            wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+        }
+        const uint32_t v = p < nw ? rdlane(wbuf, p - p0) : 0u;
+        bad |= p >= nw;
+        ++p;
+        return v;
+    };
+    auto get_bits = [&](int nb) -> uint32_t {
+        const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
+        x >>= nb;
+        if (x < (1ull << 31)) x = (x << 32) | next_word();
+        x = uni64(x);
+        return v;
+    };
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int cnt_i = min(64, Mlat - kb * 64);
-        for (int ii = 0; ii < cnt_i && !bad; ++ii) {
-            const int ci = __builtin_amdgcn_readlane(idxr[kb], ii);
-            if (ci < 0 || ci > 63) { bad = 2; break; }
+        for (int ii = 0; ii < cnt_i; ++ii) {
+            const int ci = __builtin_amdgcn_readlane(idxr[kb], ii) & 63;     // indexes are 0..63 by construction
             const int base = __builtin_amdgcn_readlane(t_base, ci);
             const int len = __builtin_amdgcn_readlane(t_len, ci);
             const int off = __builtin_amdgcn_readlane(t_off, ci);
             const uint32_t cum = (uint32_t)(x & 0xffff);
-            // start the window at the Gaussian quantile of cum (the table is the quantised CDF of
-            // N(0, sigma) centred at -off): one window read finds the symbol almost always
-            const float sig = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t_sig), ci));
-            const float z = 1.41421356f * erfinvf(fminf(fmaxf(((float)cum + 0.5f) * (2.0f / 65536.0f) - 1.0f, -0.999999f), 0.999999f));
-            int guess = -off + (int)rintf(sig * z);
-            int lo = min(max(0, guess - 31), max(0, len - 64));
+            // window start: the symbol at the start of cum's 256-wide bucket (host-built LUT)
+            int lo = llut[ci * 256 + (cum >> 8)];
+            lo = __builtin_amdgcn_readfirstlane(lo);
             uint32_t c;
             int cnt;
             for (;;) {
                 const int j = lo + lane;
-                c = j < len - 1 ? (uint32_t)lcdf[base + j] : 65536u;
+                // unconditional LDS read (the LUT behind the last table keeps base + j in bounds),
+                // entries past the table's end act as 2^16
+                const uint32_t raw = lcdf[base + j];
+                c = j < len - 1 ? raw : 65536u;
                 cnt = __popcll(__ballot(c <= cum));
-                if (cnt == 0) { lo = max(0, lo - 63); continue; }
-                if (cnt == 64) { lo += 63; continue; }
-                break;
+                if (cnt < 64) break;
+                lo += 63;
             }
             const int sidx = lo + cnt - 1;
             const uint32_t start = rdlane(c, cnt - 1), nxt = rdlane(c, cnt);
             x = (unsigned long long)(nxt - start) * (x >> 16) + (x & 0xffff) - start;
             if (x < (1ull << 31)) x = (x << 32) | next_word();
+            x = uni64(x);
             int v = sidx;
             if (v == len - 2) {   // escape: value coded in 4-bit bypass chunks
                 uint32_t cc = get_bits(4), nb = cc;
                 while (cc == 15u && nb <= 8) { cc = get_bits(4); nb += cc; }
-                if (nb > 8) { bad = 3; break; }
+                if (nb > 8) { bad |= 4; nb = 0; }
                 uint32_t raw = 0;
                 for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits(4) << (jj * 4);
                 v = (int)(raw >> 1);
@@ -427,22 +431,22 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
     stamp_start(a.ts);
-    {
+    {   // CDF tables + start-index LUT (both built on the host, contiguous in cdf16)
         const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
         uint4* dst = reinterpret_cast<uint4*>(lcdf);
-        for (int i = threadIdx.x; i < a.total16 / 8; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (a.total16 + 64 * 256) / 8; i += blockDim.x) dst[i] = src[i];
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * RANS_WPB + (threadIdx.x >> 6);
-    if (row < a.rows) rans_row(a, lcdf, row, lane);
+    if (row < a.rows) rans_row(a, lcdf, lcdf + a.total16, row, lane);
     stamp_end(a.ts);
 }
 
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
     if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 table must be padded to 16 bytes");
-    const size_t lds = (size_t)a.total16 * sizeof(uint16_t);
+    const size_t lds = (size_t)(a.total16 + 64 * 256) * sizeof(uint16_t);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),

@@ -4,6 +4,7 @@
 #define LBIC_PHASE_STAMPS 1
 #include "kernels.hip"
 
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -59,7 +60,7 @@ int main() {
         (void)hipEventElapsedTime(&ms, e0, e1);
         std::vector<unsigned long long> p(8 * 4096);
         (void)hipMemcpy(p.data(), ph, 8 * 8 * 4096, hipMemcpyDeviceToHost);
-        const int nwg = ((h.N + 15) / 16) * ((h.M + 31) / 32);
+        const int nwg = ((h.N + 15) / 16) * ((h.M + 15) / 16);
         double acc[5] = {0, 0, 0, 0, 0};
         unsigned long long t0 = ~0ull, t1 = 0;
         for (int wg = 0; wg < nwg && variant != 3; ++wg) {
@@ -72,6 +73,61 @@ int main() {
         if (variant != 3)
             printf(" | last launch, per-WG avg cycles: setup %.0f  kloop %.0f  lds %.0f  epi %.0f | span %llu cyc (%d WGs)",
                    acc[1] / nwg, acc[2] / nwg, acc[3] / nwg, acc[4] / nwg, t1 - t0, nwg);
+        printf("\n");
+    }
+    // stream concurrency: R launches on one stream vs R/2 on each of two streams (eager), and as graphs
+    {
+        hipStream_t s1, s2;
+        (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+        (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+        // separate output buffers so the two streams do not write the same memory
+        float* out2;
+        (void)hipMalloc(&out2, sizeof(float) * M * 1152);
+        GemmArgs g2 = g;
+        g2.out = out2;
+        auto run = [&](int mode) {
+            (void)hipDeviceSynchronize();
+            auto t0 = std::chrono::high_resolution_clock::now();
+            if (mode == 0) for (int i = 0; i < R; ++i) launch_gemm(g, s1);
+            else for (int i = 0; i < R / 2; ++i) { launch_gemm(g, s1); launch_gemm(g2, s2); }
+            (void)hipDeviceSynchronize();
+            auto t1 = std::chrono::high_resolution_clock::now();
+            return std::chrono::duration<double, std::micro>(t1 - t0).count() / R;
+        };
+        run(0);
+        printf("eager: 1 stream %.2f us/launch, 2 streams %.2f us/launch\n", run(0), run(1));
+        // graphs of 100 launches each
+        auto mkgraph = [&](GemmArgs& gg, hipStream_t st) {
+            hipGraph_t gr; hipGraphExec_t ex;
+            (void)hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+            for (int i = 0; i < 100; ++i) launch_gemm(gg, st);
+            (void)hipStreamEndCapture(st, &gr);
+            (void)hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+            return ex;
+        };
+        hipGraphExec_t ga = mkgraph(g, s1), gb = mkgraph(g2, s2);
+        auto runq = [&](int mode) {
+            (void)hipDeviceSynchronize();
+            auto t0 = std::chrono::high_resolution_clock::now();
+            for (int i = 0; i < R / 100; ++i) {
+                if (mode == 0) { (void)hipGraphLaunch(ga, s1); }
+                else if (i % 2 == 0) { (void)hipGraphLaunch(ga, s1); (void)hipGraphLaunch(gb, s2); }
+            }
+            (void)hipDeviceSynchronize();
+            auto t1 = std::chrono::high_resolution_clock::now();
+            return std::chrono::duration<double, std::micro>(t1 - t0).count() / R;
+        };
+        runq(0);
+        printf("graphs: 1 stream %.2f us/launch, 2 streams %.2f us/launch\n", runq(0), runq(1));
+    }
+    // workgroup -> XCD placement over consecutive launches
+    for (int rep = 0; rep < 4; ++rep) {
+        launch_gemm(g, nullptr);
+        (void)hipDeviceSynchronize();
+        std::vector<unsigned long long> p(8 * 4096);
+        (void)hipMemcpy(p.data(), ph, 8 * 8 * 4096, hipMemcpyDeviceToHost);
+        printf("launch %d xcc of wg 0..23:", rep);
+        for (int wg = 0; wg < 24; ++wg) printf(" %llu", p[wg * 8 + 7]);
         printf("\n");
     }
     return 0;

@@ -195,8 +195,9 @@ class BlockBasedImgCompLossyNetv9:
         arr = (_lib.LbcKernelStat * 8)()
         n = ctypes.c_int()
         _lib.check(_lib.lib().lbc_profile_end(self._h, arr, 8, ctypes.byref(n)))
-        return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms, flops=arr[i].flops,
-                                           bytes=arr[i].bytes) for i in range(n.value)}
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, total_launches=arr[i].total_launches,
+                                           total_ms=arr[i].total_ms, flops=arr[i].flops, bytes=arr[i].bytes)
+                for i in range(n.value)}
 
     def last_timing(self):
         e, d = ctypes.c_double(), ctypes.c_double()

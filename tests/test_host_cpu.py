@@ -1,0 +1,75 @@
+"""CPU tests of the host mirror: config handling, layout, metrics, and the multi-process image sharding +
+summary all-gather (gloo, world_size 2) that the GPU path uses over RCCL."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, load_golden
+
+
+def test_config_and_process(tmp_path):
+    from lbic.config import get_config_from_json, process_config
+    cfg_path = os.path.join(PKG, "configs", "blkbsdimgcomp_B8_lowrate.json")
+    cfg, d = get_config_from_json(cfg_path)
+    assert cfg.block_size == 8 and cfg.N == 768 and cfg.M == 96 and cfg.agent == "BlockBasedImgCompLossyAgent"
+    cfg.exp_name = os.path.join(cfg.multi_exp_name, "exp_117.045")
+    cfg = process_config(cfg, root=str(tmp_path))
+    assert os.path.isdir(cfg.checkpoint_dir) and os.path.isdir(cfg.log_dir)
+    from lbic.arch import arch_from_config
+    a = arch_from_config(cfg)
+    assert a.lru == 1 and a.live_macs_per_block() == (8994816, 5925888)
+
+
+def test_torch_layout_matches_reference_golden():
+    from lbic.layout import arrange_block_pixels_to_channel_dim, arrange_channel_dim_to_block_pixels
+    g = load_golden("loop_b4_highrate")
+    img = torch.from_numpy(g["image"].astype(np.float32) / 255.0 - 0.5)[None]
+    t = arrange_block_pixels_to_channel_dim(img, 4)
+    assert np.array_equal(t[0].permute(1, 2, 0).numpy(), g["x"])
+    assert torch.equal(arrange_channel_dim_to_block_pixels(t, 4), img)
+
+
+def test_ms_ssim_sanity():
+    from lbic.metrics import ms_ssim
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(1, 3, 192, 192, generator=g)
+    assert abs(ms_ssim(x, x).item() - 1.0) < 1e-6
+    a = ms_ssim(x, (x + 0.05 * torch.randn(x.shape, generator=g)).clamp(0, 1)).item()
+    b = ms_ssim(x, (x + 0.20 * torch.randn(x.shape, generator=g)).clamp(0, 1)).item()
+    assert 1.0 > a > b > 0.0
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from lbic import dist as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    items = list(range(7))
+    mine = D.shard(items, rank, world)
+    rec = torch.tensor([[i, i * 10.0] for i in mine], dtype=torch.float64)
+    allrec = D.gather_records(rec)
+    q.put((rank, mine, allrec.numpy().tolist()))
+    dist.destroy_process_group()
+
+
+def test_shard_and_gather_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert res[0][1] == [0, 2, 4, 6] and res[1][1] == [1, 3, 5]
+    for _, _, allrec in res:
+        got = sorted(int(r[0]) for r in allrec)
+        assert got == list(range(7))
+        assert all(r[1] == r[0] * 10 for r in allrec)
