@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    ap.add_argument("--substream-steps", type=int, default=2,
+                    help="extra steps in the opt-in per-row sub-stream format, reported apart (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,14 +122,14 @@ def main():
 
     phase = dict(encode=0.0, entropy=0.0, decode=0.0)
 
-    def step(record=False):
+    def step(record=False, fmt="reference"):
         t0 = time.perf_counter()
         r = model.compress_batch(xb)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
-        streams = model.entropy_encode(r["symbols"], r["indexes"])
+        streams = model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
         t2 = time.perf_counter()
-        z = model.decompress_batch(streams, Hb, Wb)
+        z = model.decompress_batch(streams, Hb, Wb, fmt=fmt)
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         if record:
@@ -160,6 +162,34 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+
+    # --- opt-in sub-stream format: same encoder, one rANS stream per block row, wavefront
+    #     decode.  Reported apart from the headline (which stays on the reference bitstream format).
+    sub = None
+    if args.substream_steps > 0:
+        for k in list(phase):
+            phase[k + "_ref"] = phase[k]
+            phase[k] = 0.0
+        step(fmt="rows")
+        barrier()
+        ts = time.perf_counter()
+        for i in range(args.substream_steps):
+            rs, ss, zs = step(record=True, fmt="rows")
+        barrier()
+        dts = time.perf_counter() - ts
+        if dist:
+            t = torch.tensor([dts], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dts = float(t.item())
+        sub_exact = bool(torch.equal(zs, rs["zhat"]))
+        sub = dict(value=round(world * n * H * W / (dts / args.substream_steps) / 1e6, 4),
+                   ms_per_step=round(dts / args.substream_steps * 1e3, 2), steps=args.substream_steps,
+                   bpp=round(float(np.mean([len(b) * 8.0 / (H * W) for b in ss])), 5),
+                   enc_dec_bit_exact_rank0=sub_exact,
+                   phases_ms_per_step={k: round(phase[k] / args.substream_steps * 1e3, 2) for k in
+                                       ("encode", "entropy", "decode")})
+        for k in ("encode", "entropy", "decode"):
+            phase[k] = phase.pop(k + "_ref")
 
     # --- quality / consistency of the last step (outside the timed region)
     bit_exact = bool(torch.equal(z, r["zhat"]))
@@ -237,6 +267,7 @@ def main():
         "step_algorithmic_tflop": round(step_flops / 1e12, 3),
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
         "kernels": kernels,
+        "substream_format": sub,
     }
     print(json.dumps(out), flush=True)
     if dist:

@@ -92,6 +92,15 @@ int lbc_rans_decode_host(const lbc_model *m, const uint8_t *data, size_t len, co
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 
+/* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
+ * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder
+ * format as lbc_rans_encode.  Costs 12 bytes per block row over the reference format and lets the
+ * decoder run the encoder's anti-diagonal wavefront instead of a raster loop.  sym/idx: one image. */
+int lbc_rans_encode_rows(const lbc_model *m, const int32_t *sym, const int32_t *idx, int Hb, int Wb, uint8_t **out,
+                         size_t *len);
+int lbc_decode_rows(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
+                    float *zhat_dev, void *stream);
+
 void lbc_free(void *p);
 const char *lbc_last_error(void);
 

@@ -69,12 +69,13 @@ struct Layer {
 // into a device slot {max(~start), max(end)}; one slot range per graph, zeroed at every replay
 constexpr int kSlotsPerRange = 4096;
 constexpr int kSlotU64 = 16;      // 8 XCDs x {max(~start), max(end)}
+constexpr int kRanges = 6;        // 0 encoder graph, 1..4 raster decoder lanes, 5 wavefront decoder graph
 struct Prof {
     int sample_every = 0;
     bool active = false;          // current step is sampled
     struct Rec { int cls; int slot; double flops, bytes; };
     std::vector<Rec> recs;
-    unsigned long long* slots = nullptr;   // device, kLanes + 1 ranges
+    unsigned long long* slots = nullptr;   // device, kRanges ranges
     int range = 0, next = 0;               // slot allocation inside the range being captured
     long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
     long long replays[8] = {};             // replays of each range's graph since lbc_profile_begin
@@ -135,9 +136,9 @@ struct lbc_model {
     Prof prof;
     // HIP graphs: the whole encoder wavefront (one replay per call) and, per decoder lane, one block row
     // (replayed Hb times; kernels take the row from a device counter)
-    hipGraphExec_t enc_exec = nullptr;
+    hipGraphExec_t enc_exec = nullptr, wf_exec = nullptr;
     std::vector<hipGraphExec_t> dec_exec;
-    std::vector<long long> enc_key, dec_key;
+    std::vector<long long> enc_key, dec_key, wf_key;
     DevBuf x_in, sym_buf, idx_buf, bits_buf, ctr;
     hipStream_t cap = nullptr;
 };
@@ -355,6 +356,71 @@ int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     return LBC_OK;
 }
 
+RansArgs rans_args(lbc_model* m) {
+    RansArgs r{};
+    r.cdf16 = m->cdf16_dev.as<uint16_t>();
+    r.tmeta = m->tmeta_dev.as<int>();
+    r.total16 = m->total16;
+    r.words = m->words.as<uint32_t>();
+    r.word_base = m->word_base.as<long long>();
+    r.word_count = m->word_count.as<int>();
+    r.state_x = m->st_x.as<unsigned long long>();
+    r.state_ptr = m->st_ptr.as<int>();
+    r.status = m->st_status.as<int>();
+    r.ldk = m->C4;
+    r.Mlat = m->M;
+    r.ldy = m->M;
+    r.streams_per_img = 1;
+    return r;
+}
+
+// Upload rANS (sub-)streams: concatenated words, per-stream base / count, and the initial state of each
+// (Rans64DecInit: the first two words).  The word buffer is baked into the decoder graphs, so it grows
+// with headroom to stay put across calls.
+int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, size_t>>& subs, hipStream_t s) {
+    const size_t n = subs.size();
+    std::vector<long long> base(n);
+    std::vector<int> cnt(n), ptr(n, 2);
+    std::vector<unsigned long long> x0(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (!subs[i].first || subs[i].second < 8 || (subs[i].second & 3)) return set_error(LBC_E_STREAM, "invalid bitstream");
+        if (subs[i].second / 4 > 0x7fffffff) return set_error(LBC_E_STREAM, "bitstream too long");
+        base[i] = (long long)(total / 4);
+        cnt[i] = (int)(subs[i].second / 4);
+        total += subs[i].second;
+        uint32_t w[2];
+        std::memcpy(w, subs[i].first, 8);
+        x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
+    }
+    std::vector<uint8_t> cat(total);
+    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat.data() + off, subs[i].first, subs[i].second);
+    int rc;
+    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
+    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
+    // per-stream arrays: sized by the stream count, pointers kept stable for the graphs
+    const size_t cap = std::max<size_t>(n, 64);
+    if ((rc = m->word_base.alloc(cap * sizeof(long long))) || (rc = m->word_count.alloc(cap * sizeof(int))) ||
+        (rc = m->st_x.alloc(cap * sizeof(unsigned long long))) || (rc = m->st_ptr.alloc(cap * sizeof(int))) ||
+        (rc = m->st_status.alloc(cap * sizeof(int))))
+        return rc;
+    HIPCHK(hipMemcpy(m->word_base.p, base.data(), n * sizeof(long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(m->word_count.p, cnt.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(m->st_x.p, x0.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(m->st_ptr.p, ptr.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(m->st_status.p, 0, n * sizeof(int), s));
+    return LBC_OK;
+}
+
+int check_status(lbc_model* m, size_t n, hipStream_t s) {
+    std::vector<int> status(n);
+    HIPCHK(hipMemcpyAsync(status.data(), m->st_status.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; ++i)
+        if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream (stream " + std::to_string(i) + ")");
+    return LBC_OK;
+}
+
 GemmArgs base_args(lbc_model* m, const int4* blocks, int rows, const float* x, int n_img, int Hb, int Wb) {
     GemmArgs g{};
     g.M = rows;
@@ -540,6 +606,7 @@ void lbc_destroy(lbc_model* m) {
         if (st) (void)hipStreamDestroy(st);
     if (m->prof.slots) (void)hipFree(m->prof.slots);
     if (m->enc_exec) (void)hipGraphExecDestroy(m->enc_exec);
+    if (m->wf_exec) (void)hipGraphExecDestroy(m->wf_exec);
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     delete m;
@@ -733,30 +800,9 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     int rc;
     if ((rc = prepare_device(m))) return rc;
     if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
-    // streams -> device; initial rANS state = the first two words (Rans64DecInit)
-    std::vector<long long> base(n_img);
-    std::vector<int> cnt(n_img), ptr(n_img, 2);
-    std::vector<unsigned long long> x0(n_img);
-    size_t total = 0;
-    for (int i = 0; i < n_img; ++i) {
-        if (!streams[i] || lens[i] < 8 || (lens[i] & 3)) return set_error(LBC_E_STREAM, "invalid bitstream");
-        base[i] = (long long)(total / 4);
-        cnt[i] = (int)(lens[i] / 4);
-        total += lens[i];
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(streams[i]);
-        x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
-    }
-    std::vector<uint8_t> cat(total);
-    for (int i = 0, off = 0; i < n_img; off += (int)lens[i], ++i) std::memcpy(cat.data() + off, streams[i], lens[i]);
-    // keep the stream buffer (baked into the decoder graphs) stable across calls: grow with headroom
-    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
-    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
-    if ((rc = dev_upload(m->word_base, base.data(), base.size() * sizeof(long long)))) return rc;
-    if ((rc = dev_upload(m->word_count, cnt.data(), cnt.size() * sizeof(int)))) return rc;
-    if ((rc = dev_upload(m->st_x, x0.data(), x0.size() * sizeof(unsigned long long)))) return rc;
-    if ((rc = dev_upload(m->st_ptr, ptr.data(), ptr.size() * sizeof(int)))) return rc;
-    if ((rc = m->st_status.alloc(n_img * sizeof(int)))) return rc;
-    HIPCHK(hipMemsetAsync(m->st_status.p, 0, n_img * sizeof(int), s));
+    std::vector<std::pair<const uint8_t*, size_t>> subs;
+    for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[i], lens[i]);
+    if ((rc = upload_streams(m, subs, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[2], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
     // image groups -> lanes: every lane runs its own raster chain on its own stream, so the small
@@ -780,7 +826,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             Work& w = m->lane[l];
             const int rows = g0[l + 1] - g0[l];
             if (rows > w.rows) { g_prof = nullptr; return set_error(LBC_E_STATE, "decoder lane workspace too small"); }
-            RansArgs r{};
+            RansArgs r = rans_args(m);
             r.cdf16 = m->cdf16_dev.as<uint16_t>();
             r.tmeta = m->tmeta_dev.as<int>();
             r.total16 = m->total16;
@@ -850,12 +896,118 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[3], s));
     m->dec_timed = true;
-    std::vector<int> status(n_img);
-    HIPCHK(hipMemcpyAsync(status.data(), m->st_status.p, n_img * sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (int i = 0; i < n_img; ++i)
-        if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream for image " + std::to_string(i));
+    return check_status(m, (size_t)n_img, s);
+}
+
+static const uint32_t kRowsMagic = 0x3157424Cu;   // "LBW1"
+
+int lbc_rans_encode_rows(const lbc_model* m, const int32_t* sym, const int32_t* idx, int Hb, int Wb, uint8_t** out,
+                         size_t* len) {
+    if (!m || !sym || !idx || !out || !len || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "bad argument");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    const size_t per_row = (size_t)Wb * m->M;
+    std::vector<std::vector<uint8_t>> rows(Hb);
+    for (int v = 0; v < Hb; ++v) {
+        int rc = rans_encode(m->tabs, sym + v * per_row, idx + v * per_row, per_row, rows[v]);
+        if (rc) return rc;
+    }
+    size_t total = 8 + 4 * (size_t)Hb;
+    for (auto& r : rows) total += r.size();
+    uint8_t* buf = static_cast<uint8_t*>(malloc(total));
+    uint32_t hdr[2] = {kRowsMagic, (uint32_t)Hb};
+    std::memcpy(buf, hdr, 8);
+    size_t off = 8 + 4 * (size_t)Hb;
+    for (int v = 0; v < Hb; ++v) {
+        const uint32_t n = (uint32_t)rows[v].size();
+        std::memcpy(buf + 8 + 4 * (size_t)v, &n, 4);
+        std::memcpy(buf + off, rows[v].data(), n);
+        off += n;
+    }
+    *out = buf;
+    *len = total;
     return LBC_OK;
+}
+
+int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* lens, int n_img, int Hb, int Wb,
+                    float* zhat_dev, void* stream) {
+    if (!m || !streams || !lens || !zhat_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    std::vector<std::pair<const uint8_t*, size_t>> subs;       // stream (img, v) at img * Hb + v
+    for (int i = 0; i < n_img; ++i) {
+        uint32_t hdr[2];
+        if (!streams[i] || lens[i] < 8 + 4 * (size_t)Hb) return set_error(LBC_E_STREAM, "invalid sub-stream container");
+        std::memcpy(hdr, streams[i], 8);
+        if (hdr[0] != kRowsMagic || (int)hdr[1] != Hb) return set_error(LBC_E_STREAM, "not a sub-stream container for this frame");
+        size_t off = 8 + 4 * (size_t)Hb;
+        for (int v = 0; v < Hb; ++v) {
+            uint32_t n;
+            std::memcpy(&n, streams[i] + 8 + 4 * (size_t)v, 4);
+            if (off + n > lens[i]) return set_error(LBC_E_STREAM, "truncated sub-stream container");
+            subs.emplace_back(streams[i] + off, (size_t)n);
+            off += n;
+        }
+    }
+    if ((rc = upload_streams(m, subs, s))) return rc;
+    // the whole anti-diagonal wavefront (the encoder's schedule) as one graph: per step, context net of
+    // every block on the diagonal -> one wave per (image, block row) decodes that row's next block ->
+    // decoder transform of every block
+    const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->words.p, (long long)m->zpad.p,
+                                        (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
+                                        (long long)m->st_x.p, m->prof.sample_every};
+    if (!m->wf_exec || key != m->wf_key) {
+        if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
+        Work& w = m->lane[0];
+        HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
+        int crc = prof_range_begin(&m->prof, kRanges - 1, m->cap);
+        drop_recs(m->prof, kRanges - 1);
+        const int4* blocks = m->blocks_enc.as<int4>();
+        g_prof = &m->prof;
+        for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
+            m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
+            const int rows = m->step_cnt[t];
+            GemmArgs g = base_args(m, blocks + m->step_off[t], rows, nullptr, n_img, Hb, Wb);
+            crc = run_ctx(m, w, g, true, m->cap);
+            RansArgs r = rans_args(m);
+            r.idx = w.idx.as<int32_t>();
+            r.ksi = w.ksi.as<float>();
+            r.yq = w.yq.as<float>();
+            r.rows = rows;
+            r.blocks = blocks + m->step_off[t];
+            r.streams_per_img = Hb;
+            r.ts = m->prof.active ? m->prof.take() : nullptr;
+            m->prof.per_replay[kRanges - 1][2] += 1;
+            if (!crc) crc = launch_rans_decode(r, m->cap);
+            if (!crc && r.ts) {
+                const double b = (double)m->total16 * 2 * ((rows + 7) / 8) + 12.0 * rows * m->M;
+                m->prof.recs.push_back({2, (int)((r.ts - m->prof.slots) / kSlotU64), 0.0, b});
+            }
+            if (!crc) crc = run_dec(m, w, g, m->cap);
+        }
+        m->prof.active = false;
+        g_prof = nullptr;
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(m->cap, &graph);
+        if (crc) { if (graph) (void)hipGraphDestroy(graph); return crc; }
+        if (e != hipSuccess) return set_error(LBC_E_HIP, std::string("wavefront decoder capture: ") + hipGetErrorString(e));
+        const hipError_t ei = hipGraphInstantiate(&m->wf_exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return set_error(LBC_E_HIP, std::string("wavefront decoder instantiate: ") + hipGetErrorString(ei));
+        m->wf_key = key;
+    }
+    HIPCHK(hipEventRecord(m->ev[2], s));
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    HIPCHK(hipGraphLaunch(m->wf_exec, s));
+    m->prof.replays[kRanges - 1] += 1;
+    if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
+    HIPCHK(hipEventRecord(m->ev[3], s));
+    m->dec_timed = true;
+    return check_status(m, subs.size(), s);
 }
 
 int lbc_profile_begin(lbc_model* m, int sample_every) {
@@ -863,8 +1015,8 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
     Prof& p = m->prof;
     if (sample_every && !p.slots) {
         HIPCHK(hipSetDevice(m->cfg.device));
-        HIPCHK(hipMalloc(&p.slots, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
-        HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1)));
+        HIPCHK(hipMalloc(&p.slots, 8 * kSlotU64 * (size_t)kSlotsPerRange * kRanges));
+        HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * kRanges));
     }
     // sample_every is part of the graph keys: a change re-captures (and re-creates the sample records);
     // an unchanged value only restarts the launch counting
@@ -884,7 +1036,7 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
     for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", kKernelNames[c]);
     if (p.slots && !p.recs.empty()) {
         HIPCHK(hipDeviceSynchronize());
-        std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * (kLanes + 1));
+        std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * kRanges);
         HIPCHK(hipMemcpy(h.data(), p.slots, h.size() * 8, hipMemcpyDeviceToHost));
         for (const auto& r : p.recs) {
             const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;

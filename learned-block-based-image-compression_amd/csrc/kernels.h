@@ -85,6 +85,7 @@ struct RansArgs {
     int ctr_stride;
     unsigned long long* ts;
     int rows;
+    int streams_per_img;     // 1: one stream per image (reference format); Hb: one per block row (sub-stream format)
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = <16,16,8>, 1 = <64,32,4>

@@ -338,7 +338,9 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {   //
 __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
                                          int lane) {
     const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
-    const int img = __builtin_amdgcn_readfirstlane(blocks[row].x);
+    const int4 blk = blocks[row];
+    // stream / state of this row: the image's (reference format) or the block row's (sub-stream format)
+    const int img = __builtin_amdgcn_readfirstlane(a.streams_per_img > 1 ? blk.x * a.streams_per_img + blk.y : blk.x);
     const int Mlat = a.Mlat;
     // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
     const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];

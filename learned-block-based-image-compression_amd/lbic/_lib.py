@@ -39,6 +39,10 @@ _SIGS = {
     "lbc_rans_decode_host": ([_P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P], ctypes.c_int),
     "lbc_decode": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                     ctypes.c_int, _P, _P], ctypes.c_int),
+    "lbc_rans_encode_rows": ([_P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P),
+                              ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "lbc_decode_rows": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
+                         ctypes.c_int, _P, _P], ctypes.c_int),
     "lbc_free": ([_P], None),
     "lbc_last_error": ([], ctypes.c_char_p),
     "lbc_last_timing": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),

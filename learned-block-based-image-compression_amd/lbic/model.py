@@ -147,19 +147,29 @@ class BlockBasedImgCompLossyNetv9:
                                          ctypes.c_void_p(stream)))
         return dict(zhat=zhat, symbols=sym, indexes=idx, bits=bits)
 
-    def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor, workers: int = 0) -> List[bytes]:
-        """BufferedRansEncoder per image (host C++, one stream per image as in the reference),
-        symbols/indexes [n, L] (any device).  Images are coded on parallel host threads (ctypes drops the
-        GIL during the call)."""
+    def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor, workers: int = 0, fmt: str = "reference",
+                       Hb: int = 0, Wb: int = 0) -> List[bytes]:
+        """BufferedRansEncoder per image (host C++), symbols/indexes [n, L] (any device).  fmt "reference":
+        one stream per image as in the reference; fmt "rows": the opt-in sub-stream container (one stream per
+        block row, lbc_rans_encode_rows; needs Hb, Wb).  Images are coded on parallel host threads
+        (ctypes drops the GIL during the call)."""
+        if fmt not in ("reference", "rows"):
+            raise ValueError(f"unknown bitstream format {fmt!r}")
         s = symbols.to("cpu", torch.int32).contiguous().numpy()
         i = indexes.to("cpu", torch.int32).contiguous().numpy()
         L = _lib.lib()
+        if fmt == "rows" and Hb * Wb * self.arch.M != s.shape[1]:
+            raise ValueError("fmt='rows' needs the frame's Hb, Wb")
 
         def one(k):
             p = ctypes.c_void_p()
             ln = ctypes.c_size_t()
-            _lib.check(L.lbc_rans_encode(self._h, _lib.ptr(s[k]), _lib.ptr(i[k]), s.shape[1], ctypes.byref(p),
-                                         ctypes.byref(ln)))
+            if fmt == "rows":
+                _lib.check(L.lbc_rans_encode_rows(self._h, _lib.ptr(s[k]), _lib.ptr(i[k]), Hb, Wb, ctypes.byref(p),
+                                                  ctypes.byref(ln)))
+            else:
+                _lib.check(L.lbc_rans_encode(self._h, _lib.ptr(s[k]), _lib.ptr(i[k]), s.shape[1], ctypes.byref(p),
+                                             ctypes.byref(ln)))
             b = ctypes.string_at(p, ln.value)
             L.lbc_free(p)
             return b
@@ -174,8 +184,12 @@ class BlockBasedImgCompLossyNetv9:
             self._pool_workers = workers
         return list(self._pool.map(one, range(n)))
 
-    def decompress_batch(self, streams: Sequence[bytes], Hb: int, Wb: int) -> torch.Tensor:
-        """Decode n bitstreams of Hb x Wb blocks on the GPU -> zhat [n, Hb, Wb, 3B^2]."""
+    def decompress_batch(self, streams: Sequence[bytes], Hb: int, Wb: int, fmt: str = "reference") -> torch.Tensor:
+        """Decode n bitstreams of Hb x Wb blocks on the GPU -> zhat [n, Hb, Wb, 3B^2].  fmt "reference": raster
+        decode of one stream per image (the reference format); "rows": wavefront decode of the sub-stream
+        containers of entropy_encode(fmt="rows")."""
+        if fmt not in ("reference", "rows"):
+            raise ValueError(f"unknown bitstream format {fmt!r}")
         self._check_ready()
         n = len(streams)
         bufs = [ctypes.create_string_buffer(bytes(s), len(s)) for s in streams]
@@ -183,7 +197,8 @@ class BlockBasedImgCompLossyNetv9:
         lens = (ctypes.c_size_t * n)(*[len(s) for s in streams])
         zhat = torch.empty((n, Hb, Wb, self.arch.cx), dtype=torch.float32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().lbc_decode(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
+        fn = _lib.lib().lbc_decode_rows if fmt == "rows" else _lib.lib().lbc_decode
+        _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
     def profile_begin(self, sample_every: int):
