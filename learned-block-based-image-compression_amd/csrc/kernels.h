@@ -27,6 +27,7 @@ struct Seg {                 // one K-range of the A operand: K columns [k0, k1)
     int ld;                  // SEG_DENSE row stride (floats)
     int dy, dx;              // SEG_ZTAP: tap offset relative to the output position
     int k0, k1;
+    int zs, xs, tap;         // set by launch_gemm: row offset = r*ld + zs*zrow + xs*xrow + tap (no branches)
 };
 
 struct Geo {
@@ -62,6 +63,7 @@ struct GemmArgs {
     float* bits;
     int HW;
     Geo geo;
+    int xcd_map;             // experiment: column tile t on XCD t % 8
 };
 
 struct RansArgs {

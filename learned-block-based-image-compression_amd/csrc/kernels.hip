@@ -48,10 +48,12 @@ __device__ __forceinline__ void stamp_end(unsigned long long* ts) {
 #ifdef LBIC_PHASE_STAMPS
 // diagnostic build only (csrc/microbench.hip): per-workgroup s_memtime at phase boundaries
 __device__ unsigned long long* g_phase;
+// (launch slot = g.ctr_stride, which the microbenchmark's dense-only launches do not otherwise use)
 #define PHASE(i)                                                                                  \
     do {                                                                                          \
-        if (threadIdx.x == 0) g_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
-        if (threadIdx.x == 0 && (i) == 0) g_phase[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + 7] = xcc_id(); \
+        const long ph_ = ((long)g.ctr_stride * 4096 + blockIdx.y * gridDim.x + blockIdx.x) * 8;   \
+        if (threadIdx.x == 0) g_phase[ph_ + (i)] = __builtin_amdgcn_s_memtime();                   \
+        if (threadIdx.x == 0 && (i) == 0) g_phase[ph_ + 7] = xcc_id();                            \
     } while (0)
 #else
 #define PHASE(i) do {} while (0)
@@ -69,6 +71,61 @@ __device__ __forceinline__ int scale_index(float s, const float* table) {
 __device__ __forceinline__ float std_cum(float x) {
     // _standardized_cumulative (entropy_layers_cai.py:569-573)
     return 0.5f * erfcf(-0.70710677f * x);
+}
+
+// Output element (row, col) of a GEMM from its slice-ordered sum v: bias + the layer's epilogue.  Shared by
+// both GEMM kernels so that they compute bit-identical values.
+// bcol = bias[col]; xv = the GDN input x[row][col] (GDN / IGDN only), both loaded by the caller.
+__device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const int4* blocks, float bcol,
+                                         float xv) {
+    switch (g.epi) {
+        case EPI_BIAS:
+            g.out[(long)row * g.ldo + col] = v + bcol;
+            break;
+        case EPI_LEAKY: {
+            const float t = v + bcol;
+            g.out[(long)row * g.ldo + col] = t > 0.f ? t : t * 0.01f;
+            break;
+        }
+        case EPI_GDN:
+        case EPI_IGDN: {
+            const float norm = v + bcol;
+            const float sq = __fsqrt_rn(norm);
+            g.out[(long)row * g.ldo + col] = g.epi == EPI_GDN ? xv * __fdiv_rn(1.0f, sq) : xv * sq;
+            break;
+        }
+        case EPI_QUANT: {
+            const float y = v + bcol;
+            const float scale = g.ksi[(long)row * g.ldk + col];
+            const float mean = g.ksi[(long)row * g.ldk + g.Mlat + col];
+            const float d = y - mean;
+            const int sym = (int)rintf(d);               // torch.round: half to even
+            const float yq = (float)sym + mean;
+            g.out[(long)row * g.ldo + col] = yq;
+            const int4 b = blocks[row];
+            const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
+            g.sym[pos] = sym;
+            g.idx[pos] = scale_index(scale, g.table);
+            if (g.bits) {
+                const float av = fabsf(yq - mean), sb = fmaxf(scale, 0.11f);
+                const float lik = std_cum((0.5f - av) / sb) - std_cum((-0.5f - av) / sb);
+                g.bits[pos] = -log2f(fmaxf(lik, 1e-9f));
+            }
+            break;
+        }
+        case EPI_CTXIDX: {
+            const float t = v + bcol;
+            g.out[(long)row * g.ldo + col] = t;
+            if (col < g.Mlat) g.idx[(long)row * g.Mlat + col] = scale_index(t, g.table);
+            break;
+        }
+        case EPI_CLAMPZ: {
+            const float t = fminf(fmaxf(v + bcol, -0.5f), 0.5f);
+            const int4 b = blocks[row];
+            g.geo.zpad[((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col] = t;
+            break;
+        }
+    }
 }
 
 // A / W fragments of one 16-wide k-block for this lane (operand maps: the packing comment in codec.hip)
@@ -101,7 +158,7 @@ __device__ __forceinline__ void load_kb(const GemmArgs& g, int kb, int nb0, cons
     for (int s = 0; s < MS; ++s) o[s] = R.off[0][s];
 #pragma unroll
     for (int t = 1; t < MAXSEG; ++t) {
-        const bool in = t < g.nseg && k >= g.seg[t].k0;     // wave-uniform
+        const bool in = k >= g.seg[t].k0;     // wave-uniform (unused segments: k0 past K)
         base = in ? g.seg[t].base : base;
         k0 = in ? g.seg[t].k0 : k0;
 #pragma unroll
@@ -155,7 +212,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         const int xrow = ((b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
 #pragma unroll
         for (int t = 0; t < MAXSEG; ++t) {
-            const Seg& sg = g.seg[t < g.nseg ? t : 0];
+            const Seg& sg = g.seg[t];
             R.off[t][s] = sg.kind == SEG_DENSE ? r * sg.ld
                         : sg.kind == SEG_ZTAP ? zrow + (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : xrow;
         }
@@ -226,57 +283,167 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         const int row = m0 + (sj / NS) * 16 + (l >> 4) * 4 + r;
         const int col = n0 + (sj % NS) * 16 + (l & 15);
         if (row >= g.M || col >= g.N) continue;
-        switch (g.epi) {
-            case EPI_BIAS:
-                g.out[(long)row * g.ldo + col] = v + g.bias[col];
-                break;
-            case EPI_LEAKY: {
-                const float t = v + g.bias[col];
-                g.out[(long)row * g.ldo + col] = t > 0.f ? t : t * 0.01f;
-                break;
-            }
-            case EPI_GDN:
-            case EPI_IGDN: {
-                const float norm = v + g.bias[col];
-                const float xv = g.gx[(long)row * g.ldx + col];
-                const float sq = __fsqrt_rn(norm);
-                g.out[(long)row * g.ldo + col] = g.epi == EPI_GDN ? xv * __fdiv_rn(1.0f, sq) : xv * sq;
-                break;
-            }
-            case EPI_QUANT: {
-                const float y = v + g.bias[col];
-                const float scale = g.ksi[(long)row * g.ldk + col];
-                const float mean = g.ksi[(long)row * g.ldk + g.Mlat + col];
-                const float d = y - mean;
-                const int sym = (int)rintf(d);               // torch.round: half to even
-                const float yq = (float)sym + mean;
-                g.out[(long)row * g.ldo + col] = yq;
-                const int4 b = blocks[row];
-                const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
-                g.sym[pos] = sym;
-                g.idx[pos] = scale_index(scale, g.table);
-                if (g.bits) {
-                    const float av = fabsf(yq - mean), sb = fmaxf(scale, 0.11f);
-                    const float lik = std_cum((0.5f - av) / sb) - std_cum((-0.5f - av) / sb);
-                    g.bits[pos] = -log2f(fmaxf(lik, 1e-9f));
-                }
-                break;
-            }
-            case EPI_CTXIDX: {
-                const float t = v + g.bias[col];
-                g.out[(long)row * g.ldo + col] = t;
-                if (col < g.Mlat) g.idx[(long)row * g.Mlat + col] = scale_index(t, g.table);
-                break;
-            }
-            case EPI_CLAMPZ: {
-                const float t = fminf(fmaxf(v + g.bias[col], -0.5f), 0.5f);
-                const int4 b = blocks[row];
-                g.geo.zpad[((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col] = t;
-                break;
-            }
-        }
+        const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
+        epilogue(g, v, row, col, blocks, g.bias[col], gdn ? g.gx[(long)row * g.ldx + col] : 0.f);
     }
     PHASE(4);
+    stamp_end(g.ts);
+}
+
+// Small-M GEMM (the decoder's per-step batch, M = n_img rows, and the wavefront's ramp steps): one
+// 16 x 16 output tile per workgroup, 8 waves = the 8 K slices, one slice per wave.  Latency-shaped:
+// every weight and activation fragment of a slice is requested before the first MFMA (the weights
+// first: they need nothing but the kernel arguments), and bias / GDN input of the epilogue at the start
+// too, so a launch costs about one memory round trip plus the slice's dependent MFMA chain.  The slice
+// length L (k-blocks) is dispatched to a fully unrolled body, so no load sits behind a branch.  Slices,
+// chain order and the slice-ordered sum are those of k_gemm: results are bit-identical to it.
+typedef const float __attribute__((address_space(1)))* gfloat_p;   // global (not flat) loads
+
+struct SRow {            // per-lane A addressing of every segment, computed once per launch
+    gfloat_p base[MAXSEG];
+    int k0[MAXSEG];
+    int off[MAXSEG];    // element offset of this lane's row in segment t, minus k0 (plus q4)
+};
+
+// this lane's A row: the row, its block (img, v, h) when a segment or the epilogue needs it, and its
+// context position; the block load is issued here and waited for only in small_offsets
+struct SBlk {
+    int r, dy, dx;
+    int4 b;
+};
+
+__device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, const int4* blocks) {
+    SBlk s;
+    s.r = min(m0 + (lane & 15), g.M - 1);
+    int m = s.r;
+    s.dy = s.dx = 0;
+    if (g.P > 1) {
+        m = s.r / g.P;
+        const int p = s.r - m * g.P;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {         // static indices only (a per-lane index would copy g to scratch)
+            s.dy = p == q ? g.pos_dy[q] : s.dy;
+            s.dx = p == q ? g.pos_dx[q] : s.dx;
+        }
+    }
+    s.b = blocks[m];     // unconditional (a branch here costs a full vmcnt drain); unused by dense-only GEMMs
+    return s;
+}
+
+__device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, int lane, SRow& s) {
+    const int4 b = k.b;
+    const int zrow = ((b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx) * g.geo.Cx;
+    const int xrow = ((b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
+    const int q4 = (lane >> 4) * 4;
+#pragma unroll
+    for (int t = 0; t < MAXSEG; ++t) {
+        const Seg& sg = g.seg[t];
+        s.base[t] = (gfloat_p)sg.base;
+        s.k0[t] = sg.k0;
+        // opaque from here on: the per-k-block selects pick values, not kernel-argument addresses
+        // (a selected address would become one dependent scalar load per k-block)
+        asm volatile("" : "+s"(s.base[t]), "+s"(s.k0[t]));
+        s.off[t] = k.r * sg.ld + sg.zs * zrow + sg.xs * xrow + sg.tap - sg.k0 + q4;
+    }
+}
+
+// A fragment of k-block kb (elements kb*16 + q4 .. +3 of this lane's row)
+__device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
+    const int k = kb << 4;
+    gfloat_p base = rw.base[0];
+    int o = rw.off[0];
+#pragma unroll
+    for (int t = 1; t < MAXSEG; ++t) {
+        const bool in = k >= rw.k0[t];     // wave-uniform; unused segments have k0 past K
+        base = in ? rw.base[t] : base;
+        o = in ? rw.off[t] : o;
+    }
+    return *reinterpret_cast<const f4 __attribute__((address_space(1)))*>(base + o + k);
+}
+
+// k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
+// differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
+// selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
+template <int L>
+__device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const int4* blocks,
+                                          f4 acc) {
+    constexpr int LL = L + 1;
+    const int nkb = g.K >> 4;
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    f4 w[LL], a[LL];
+    const SBlk bk = small_blk(g, m0, lane, blocks);      // issued first: the A addresses wait for it
+#pragma unroll
+    for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
+    SRow rw;
+    small_offsets(g, bk, lane, rw);
+    PHASE(1);
+#pragma unroll
+    for (int c = 0; c < LL; ++c) a[c] = small_a(rw, min(kb0 + c, nkb - 1));
+    // keep every load above the MFMAs (the scheduler would otherwise sink each one next to its first use
+    // and wait for it there: one memory round trip per k-block)
+    __builtin_amdgcn_sched_barrier(0);
+    PHASE(2);
+#pragma unroll
+    for (int c = 0; c < LL; ++c) {
+        f4 av = a[c];
+        if (g.square_a) av = av * av;
+        f4 t = acc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+        acc = c < n ? t : acc;
+    }
+    return acc;
+}
+
+// L = (K/16) / 8 k-blocks per slice (each slice L or L+1); L > 12: chunks of 12
+template <int L>
+__global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int nt = blockIdx.x;
+    if (g.xcd_map) {      // column tile t runs on XCD t % 8 (assumes round-robin dispatch; experiment only)
+        nt = xcc_id() + 8 * (blockIdx.x >> 3);
+        if (nt * 16 >= g.N) return;
+    }
+    const int n0 = nt * 16, m0 = blockIdx.y * 16;
+    stamp_start(g.ts);
+    PHASE(0);
+    // epilogue operands of this thread's output element (threads 0..255; the rest load a duplicate)
+    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
+    const int erow = min(m0 + (el >> 4) * 4 + er, g.M - 1), ecol = min(n0 + (el & 15), g.N - 1);
+    const float bcol = g.bias[ecol];
+    const float xv = (g.epi == EPI_GDN || g.epi == EPI_IGDN) ? g.gx[(long)erow * g.ldx + ecol] : 0.f;
+
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
+    const int4* blocks = g.blocks;
+    if (g.need_blocks && g.ctr) {
+        // scalar load: stays out of the vector-memory counter, so no weight load waits behind it
+        int c;
+        asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c) : "s"(g.ctr) : "memory");
+        blocks += (long)c * g.ctr_stride;
+    }
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (L <= 12) {
+        acc = small_slice<L>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
+    } else {
+        for (int c0 = kb0; c0 < kb1; c0 += 12) acc = small_slice<11>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
+    }
+    PHASE(3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave * 256 + i * 64 + lane] = acc[i];
+    __syncthreads();
+    PHASE(4);
+    if (threadIdx.x < 256) {
+        const int e = threadIdx.x;
+        float v = red[e];
+#pragma unroll
+        for (int i = 1; i < KSPLIT; ++i) v += red[i * 256 + e];
+        const int row = m0 + (el >> 4) * 4 + er, col = n0 + (el & 15);
+        if (row < g.M && col < g.N) epilogue(g, v, row, col, blocks, bcol, xv);
+    }
+    PHASE(5);
     stamp_end(g.ts);
 }
 
@@ -309,9 +476,28 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
             return set_error(LBC_E_ARG, "bad GEMM segment");
     }
     if (!g.W || !g.bias || !g.blocks || g.P < 1 || g.P > 5) return set_error(LBC_E_ARG, "bad GEMM arguments");
-    if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): more, lighter tiles
+    for (int t = 0; t < g.nseg; ++t) {            // branch-free row offset: r*ld + zs*zrow + xs*xrow + tap
+        Seg& sg = g.seg[t];
+        sg.zs = sg.kind == SEG_ZTAP;
+        sg.xs = sg.kind == SEG_X;
+        sg.tap = sg.kind == SEG_ZTAP ? (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : 0;
+        if (sg.kind != SEG_DENSE) sg.ld = 0;
+    }
+    for (int t = g.nseg; t < MAXSEG; ++t) {       // unused segments: never selected (k0 past every k)
+        g.seg[t] = g.seg[0];
+        g.seg[t].k0 = g.seg[t].k1 = 1 << 30;
+    }
+    if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
-        return launch_cfg<16, 16, 8, 4>(g, s);
+        dim3 grid(g.xcd_map ? ((g.N + 127) / 128) * 8 : (g.N + 15) / 16, (g.M + 15) / 16);
+        switch ((g.K >> 4) / KSPLIT) {
+#define LBIC_L(L) case L: hipLaunchKernelGGL(k_gemm_s<L>, grid, dim3(512), 0, s, g); break;
+            LBIC_L(0) LBIC_L(1) LBIC_L(2) LBIC_L(3) LBIC_L(4) LBIC_L(5) LBIC_L(6)
+            LBIC_L(7) LBIC_L(8) LBIC_L(9) LBIC_L(10) LBIC_L(11) LBIC_L(12)
+#undef LBIC_L
+            default: hipLaunchKernelGGL(k_gemm_s<13>, grid, dim3(512), 0, s, g);
+        }
+        return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
     }
     if (cfg_id) *cfg_id = 1;
     return launch_cfg<64, 32, 4, 2>(g, s);
@@ -325,7 +511,10 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
 // window, and the next 64 stream words sit lane-distributed in a register (renormalisation is a
 // readlane, not a dependent global load).  The 64-bit state is wave-uniform.  Output:
 // y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
-constexpr int RANS_WPB = 8;      // waves (images) per workgroup
+#ifndef LBIC_RANS_WPB
+#define LBIC_RANS_WPB 8
+#endif
+constexpr int RANS_WPB = LBIC_RANS_WPB;   // waves (images) per workgroup
 constexpr int RANS_MAXLAT = 256; // Mlat <= 4 * 64
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }

@@ -14,7 +14,7 @@ int set_error(int code, const std::string& msg) { fprintf(stderr, "%s\n", msg.c_
 using namespace lbic;
 
 int main(int argc, char** argv) {
-    const int n_img = argc > 1 ? atoi(argv[1]) : 32, M = 96, steps = 64;
+    const int n_img = argc > 1 ? atoi(argv[1]) : 32, M = argc > 2 ? atoi(argv[2]) : 96, steps = 64;
     // Gaussian tables exactly as GaussianConditional.update builds them (double erfc here; fine for a bench)
     EntropyTables t;
     t.n_tables = 64;
