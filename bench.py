@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0.  See DESIGN.md for the roofline definitions.
 """
 import argparse
 import json
+import re
 import math
 import os
 import sys
@@ -237,8 +238,16 @@ def main():
             ach, peak, unit, bound = s["flops"] / t_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
         else:
             ach, peak, unit, bound = s["bytes"] / t_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+        traffic = None
+        tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/pmc_summary.py), HBM bytes per launch
+            with open(tfile) as fh:
+                pm = json.load(fh)
+            fam = re.sub(r"<.*>$", "", dom)
+            if fam in pm and "hbm_bytes_per_dispatch" in pm[fam]:
+                traffic = round(pm[fam]["hbm_bytes_per_dispatch"])
         roof = dict(kernel=dom, bound=bound, achieved=round(ach, 3), peak=peak, unit=unit,
-                    frac=round(ach / peak, 5), traffic=None,
+                    frac=round(ach / peak, 5), traffic=traffic,
                     avg_launch_us=round(s["total_ms"] / s["launches"] * 1e3, 3),
                     algorithmic_per_launch=dict(flops=s["flops"] / s["launches"], bytes=s["bytes"] / s["launches"]),
                     arithmetic_intensity=round(ai, 2))
