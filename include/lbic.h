@@ -76,6 +76,15 @@ int lbc_set_entropy_tables(lbc_model *m, const float *scale_table, int n_tables,
 int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, float *zhat_dev,
                int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, void *stream);
 
+/* Teacher-forced forward pass, BlockBasedImgCompLossyNetv4.forward(zhat, x) inherited by v9
+ * (graphs/models/BlockBasedImgCompLossy_net.py:90-106), eval mode: every block sees the GIVEN zhat
+ * (no closed loop), with the full-frame 'same' convolutions of the reference's nn.Sequential layers.
+ * x_dev, zhat_dev: [n_img][Hb][Wb][3B^2] fp32 on the device.  Outputs: xhat_dev [n_img][Hb][Wb][3B^2]
+ * (inverse transform of the dequantized latent, not clamped) and info_dev [n_img][Hb][Wb][M] =
+ * -log2 of the Gaussian likelihood with the 1e-9 lower bound (entropy_layers_cai.py:615-647). */
+int lbc_forward(lbc_model *m, const float *x_dev, const float *zhat_dev, int n_img, int Hb, int Wb, float *xhat_dev,
+                float *info_dev, void *stream);
+
 /* BufferedRansEncoder.encode_with_indexes + flush (net:328,359-360), host C++, one image.
  * *out is allocated by the library (release with lbc_free). */
 int lbc_rans_encode(const lbc_model *m, const int32_t *sym, const int32_t *idx, size_t n, uint8_t **out,

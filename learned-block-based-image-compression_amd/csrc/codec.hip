@@ -484,13 +484,15 @@ int run_gdn(GemmArgs g, const Layer& L, const float* in, int ld, bool inverse, f
 }
 
 // context net (get_meanscale_fast, net:389-398) for the rows of `g`; the last layer's epilogue is
-// plain (encode) or also emits the scale indexes (decode).
-int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s) {
+// plain (encode) or also emits the scale indexes (decode).  frame_pad: forward()'s full-frame semantics
+// (get_meanscale as nn.Sequential, net:57-65): the layer-0 map is zero outside the frame.
+int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, bool frame_pad = false) {
     int rc;
     {
         GemmArgs c = g;
         c.nseg = 0;
         c.square_a = 0;
+        c.zero_oob = frame_pad && m->P > 1;
         c.P = m->P;
         c.M = g.M * m->P;
         for (int p = 0; p < m->P; ++p) {
@@ -511,8 +513,9 @@ int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s) {
                      m->C4, s);
 }
 
-// decoder transform (inverse_prtr_fast, net:384-387) + clamp + write-back into zpad (net:357)
-int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s) {
+// decoder transform (inverse_prtr_fast, net:384-387) + clamp + write-back into zpad (net:357); with
+// xhat: the unclamped output scattered to xhat[img][v][h] instead (forward(), net:104)
+int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s, float* xhat = nullptr) {
     int rc;
     {
         GemmArgs c = g;
@@ -530,6 +533,7 @@ int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s) {
     if ((rc = run_gdn(g, m->ig1, d0, W, true, d1, s))) return rc;
     if ((rc = run_dense(g, m->d2, d1, W, EPI_BIAS, d0, W, s))) return rc;
     if ((rc = run_gdn(g, m->ig2, d0, W, true, d1, s))) return rc;
+    if (xhat) return run_dense(g, m->d3, d1, W, EPI_SCATTER, xhat, m->Cx, s);   // forward(): xhat, not clamped
     return run_dense(g, m->d3, d1, W, EPI_CLAMPZ, nullptr, 0, s);
 }
 
@@ -769,6 +773,35 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
     HIPCHK(hipEventRecord(m->ev[1], s));
     m->enc_timed = true;
     return LBC_OK;
+}
+
+int lbc_forward(lbc_model* m, const float* x_dev, const float* zhat_dev, int n_img, int Hb, int Wb, float* xhat_dev,
+                float* info_dev, void* stream) {
+    if (!m || !x_dev || !zhat_dev || !xhat_dev || !info_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    const size_t nsym = (size_t)n_img * Hb * Wb * m->M;
+    if ((rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4))) return rc;
+    // teacher forcing: the given zhat is the reconstruction every block sees (zero border as before)
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    if ((rc = launch_fill_interior(zhat_dev, m->zpad.as<float>(), n_img, Hb, Wb, m->Cx, s))) return rc;
+    // every block is independent here: chunks of the encoder workspace's row capacity, eager launches
+    Work& w = m->lane[0];
+    const int total = n_img * Hb * Wb;
+    const int4* blocks = m->blocks_enc.as<int4>();    // all blocks (wavefront order; outputs go by block)
+    for (int off = 0; off < total && !rc; off += w.rows) {
+        const int cnt = std::min(w.rows, total - off);
+        GemmArgs g = base_args(m, blocks + off, cnt, x_dev, n_img, Hb, Wb);
+        if (!rc) rc = run_ctx(m, w, g, false, s, true);
+        if (!rc) rc = run_enc(m, w, g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(), info_dev, s);
+        if (!rc) rc = run_dec(m, w, g, s, xhat_dev);
+    }
+    return rc;
 }
 
 int lbc_rans_encode(const lbc_model* m, const int32_t* sym, const int32_t* idx, size_t n, uint8_t** out, size_t* len) {

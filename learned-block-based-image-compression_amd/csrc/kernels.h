@@ -19,7 +19,7 @@ constexpr int KSPLIT = 8;   // every GEMM output = ((s0 + s1) + ... + s7) + bias
                             // (large wavefront M) and the decoder (M = n_img) compute bit-identical values.
 
 enum SegKind : int { SEG_DENSE = 0, SEG_ZTAP = 1, SEG_X = 2 };
-enum Epi : int { EPI_BIAS = 0, EPI_LEAKY, EPI_GDN, EPI_IGDN, EPI_QUANT, EPI_CTXIDX, EPI_CLAMPZ };
+enum Epi : int { EPI_BIAS = 0, EPI_LEAKY, EPI_GDN, EPI_IGDN, EPI_QUANT, EPI_CTXIDX, EPI_CLAMPZ, EPI_SCATTER };
 
 struct Seg {                 // one K-range of the A operand: K columns [k0, k1)
     const float* base;       // SEG_DENSE: activations base
@@ -64,6 +64,8 @@ struct GemmArgs {
     int HW;
     Geo geo;
     int xcd_map;             // experiment: column tile t on XCD t % 8
+    int zero_oob;            // EPI_LEAKY: rows whose context position lies outside the frame are written as 0
+                             // (forward()'s zero padding of the layer-0 map, KS[1] = 3)
 };
 
 struct RansArgs {
@@ -94,5 +96,6 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // c
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
+int launch_fill_interior(const float* zin, float* zpad, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
 
 }  // namespace lbic

@@ -84,7 +84,20 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             break;
         case EPI_LEAKY: {
             const float t = v + bcol;
-            g.out[(long)row * g.ldo + col] = t > 0.f ? t : t * 0.01f;
+            float o = t > 0.f ? t : t * 0.01f;
+            if (g.zero_oob) {    // row = block * P + position; position outside the frame -> 0
+                const int m = row / g.P, p = row - m * g.P;
+                int dy = 0, dx = 0;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    dy = p == q ? g.pos_dy[q] : dy;
+                    dx = p == q ? g.pos_dx[q] : dx;
+                }
+                const int4 b = blocks[m];
+                const int vv = b.y + dy, hh = b.z + dx;
+                if (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb) o = 0.f;
+            }
+            g.out[(long)row * g.ldo + col] = o;
             break;
         }
         case EPI_GDN:
@@ -117,6 +130,11 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             const float t = v + bcol;
             g.out[(long)row * g.ldo + col] = t;
             if (col < g.Mlat) g.idx[(long)row * g.Mlat + col] = scale_index(t, g.table);
+            break;
+        }
+        case EPI_SCATTER: {   // output row of block (img, v, h) -> out[img][v][h][col] (forward()'s xhat)
+            const int4 b = blocks[row];
+            g.out[((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col] = v + bcol;
             break;
         }
         case EPI_CLAMPZ: {
@@ -463,7 +481,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
 
 int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     GemmArgs g = g0;
-    g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ;
+    g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ || g.epi == EPI_SCATTER || g.zero_oob;
     for (int t = 0; t < g.nseg && t < MAXSEG; ++t) g.need_blocks |= g.seg[t].kind != SEG_DENSE;
     if (g.M <= 0) return LBC_OK;
     if (g.K % 16 || g.K < 16) return set_error(LBC_E_ARG, "GEMM K must be a positive multiple of 16");
@@ -524,6 +542,18 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {   //
     return ((unsigned long long)hi << 32) | lo;
 }
 
+#ifdef LBIC_RANS_STAMPS
+__device__ unsigned long long* g_rdbg;
+#define RSTAMP(var)                                                                                   \
+    unsigned long long var;                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");                      \
+    __builtin_amdgcn_sched_barrier(0);
+#define RACC(k, d) acc[k] += (d)
+#else
+#define RSTAMP(var)
+#define RACC(k, d)
+#endif
 __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
                                          int lane) {
     const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
@@ -547,6 +577,9 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
         symr[kb] = 0;
     }
     int bad = 0;
+#ifdef LBIC_RANS_STAMPS
+    unsigned long long acc[4] = {0, 0, 0, 0};
+#endif
     // next stream word (lane-distributed window of 64 words; reloaded every 64 words)
     auto next_word = [&]() -> uint32_t {
         if (p - p0 >= 64) {
@@ -569,6 +602,7 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
     for (int kb = 0; kb < 4; ++kb) {
         const int cnt_i = min(64, Mlat - kb * 64);
         for (int ii = 0; ii < cnt_i; ++ii) {
+            RSTAMP(t0)
             const int ci = __builtin_amdgcn_readlane(idxr[kb], ii) & 63;     // indexes are 0..63 by construction
             const int base = __builtin_amdgcn_readlane(t_base, ci);
             const int len = __builtin_amdgcn_readlane(t_len, ci);
@@ -577,6 +611,8 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
             // window start: the symbol at the start of cum's 256-wide bucket (host-built LUT)
             int lo = llut[ci * 256 + (cum >> 8)];
             lo = __builtin_amdgcn_readfirstlane(lo);
+            RSTAMP(t1)
+            RACC(0, t1 - t0);
             uint32_t c;
             int cnt;
             for (;;) {
@@ -589,11 +625,15 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
                 if (cnt < 64) break;
                 lo += 63;
             }
+            RSTAMP(t2)
+            RACC(1, t2 - t1);
             const int sidx = lo + cnt - 1;
             const uint32_t start = rdlane(c, cnt - 1), nxt = rdlane(c, cnt);
             x = (unsigned long long)(nxt - start) * (x >> 16) + (x & 0xffff) - start;
             if (x < (1ull << 31)) x = (x << 32) | next_word();
             x = uni64(x);
+            RSTAMP(t3)
+            RACC(2, t3 - t2);
             int v = sidx;
             if (v == len - 2) {   // escape: value coded in 4-bit bypass chunks
                 uint32_t cc = get_bits(4), nb = cc;
@@ -605,12 +645,138 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
                 v = (raw & 1) ? -v - 1 : v + len - 2;
             }
             if (lane == ii) symr[kb] = v + off;
+            RSTAMP(t4)
+            RACC(3, t4 - t3);
         }
     }
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
         if (i < Mlat) a.yq[(long)row * a.ldy + i] = (float)symr[kb] + a.ksi[(long)row * a.ldk + Mlat + i];
+    }
+#ifdef LBIC_RANS_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 4; ++k) g_rdbg[row * 4 + k] = acc[k];
+#endif
+    if (lane == 0) {
+        a.state_x[img] = x;
+        a.state_ptr[img] = p;
+        if (bad) a.status[img] = bad;
+    }
+}
+
+// Speculative form of rans_row (same stream semantics, same outputs).  Per symbol every lane j of the
+// CDF window [lo, lo+64) computes the state that WOULD follow if the symbol were lo+j, renormalisation
+// included, in vector registers while the ballot finds the actual symbol; the state then comes back
+// with three v_readlane.  The start-index LUT rows of RANS_CH symbols sit in registers (one bucket
+// lookup = two v_readlane), and the per-symbol table data (base, length) is read from lane-distributed
+// registers off the critical path.  Dependent chain per symbol: bucket -> one LDS window read ->
+// compare/ballot (beside the speculative state) -> readlane.
+constexpr int RANS_CH = 32;
+
+__device__ __forceinline__ void rans_row_spec(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
+                                              int lane) {
+    int img = row;
+    if (a.streams_per_img > 1) {
+        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
+        const int4 blk = blocks[row];
+        img = blk.x * a.streams_per_img + blk.y;
+    }
+    img = __builtin_amdgcn_readfirstlane(img);
+    const int Mlat = a.Mlat;
+    const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
+    unsigned long long x = uni64(a.state_x[img]);
+    int p = __builtin_amdgcn_readfirstlane(a.state_ptr[img]);
+    const uint32_t* w = a.words + a.word_base[img];
+    const int nw = __builtin_amdgcn_readfirstlane(a.word_count[img]);
+    int p0 = p;
+    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+    uint32_t wnext = rdlane(wbuf, 0);
+    int bad = 0;
+    auto get_bits = [&](int nb) -> uint32_t {      // bypass chunks (escapes only)
+        const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
+        x >>= nb;
+        if (x < (1ull << 31)) {
+            bad |= p >= nw;
+            x = (x << 32) | wnext;
+            ++p;
+            if (p - p0 >= 64) {
+                p0 = p;
+                wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+            }
+            wnext = p < nw ? rdlane(wbuf, p - p0) : 0u;
+        }
+        x = uni64(x);
+        return v;
+    };
+    for (int i0 = 0; i0 < Mlat; i0 += RANS_CH) {
+        const int cnt = min(RANS_CH, Mlat - i0);
+        const int ci_l = lane < cnt ? (a.idx[(long)row * Mlat + i0 + lane] & 63) : 0;
+        // lane i: table data of symbol i0+i
+        const int base_l = __shfl(t_base, ci_l), len_l = __shfl(t_len, ci_l), off_l = __shfl(t_off, ci_l);
+        uint32_t L0[RANS_CH], L1[RANS_CH];
+#pragma unroll
+        for (int i = 0; i < RANS_CH; ++i) {
+            const int ci = __builtin_amdgcn_readlane(ci_l, i);
+            const uint2 v = *reinterpret_cast<const uint2*>(llut + ci * 256 + lane * 4);
+            L0[i] = v.x;
+            L1[i] = v.y;
+        }
+        int symv = 0;
+#pragma unroll
+        for (int i = 0; i < RANS_CH; ++i) {
+            if (i < cnt) {
+                const int base = __builtin_amdgcn_readlane(base_l, i);
+                const int len = __builtin_amdgcn_readlane(len_l, i);
+                const uint32_t cum = (uint32_t)x & 0xffffu;
+                const unsigned long long xq = x >> 16;
+                const uint32_t e = cum >> 8;
+                const uint32_t w0 = rdlane(L0[i], e >> 2), w1 = rdlane(L1[i], e >> 2);
+                const uint32_t ww = (e & 2) ? w1 : w0;
+                int lo = (int)((ww >> ((e & 1) * 16)) & 0xffffu);
+                int n;
+                unsigned long long xr;
+                uint32_t rnv;
+                for (;;) {
+                    const int j = lo + lane;
+                    const uint32_t r0 = lcdf[base + j], r1 = lcdf[base + j + 1];
+                    const uint32_t c0 = j < len - 1 ? r0 : 65536u;
+                    const uint32_t c1 = j + 1 < len - 1 ? r1 : 65536u;
+                    n = __popcll(__ballot(c0 <= cum));
+                    // speculative next state of lane j's symbol (only lane n-1's is used)
+                    const unsigned long long xn = (unsigned long long)(c1 - c0) * xq + (cum - c0);
+                    const bool rn = xn < (1ull << 31);
+                    xr = rn ? ((xn << 32) | wnext) : xn;
+                    rnv = rn ? 1u : 0u;
+                    if (__builtin_expect(n < 64, 1)) break;
+                    lo += 64;      // interval beyond this window (distribution tails)
+                }
+                const uint32_t xlo = rdlane((uint32_t)xr, n - 1), xhi = rdlane((uint32_t)(xr >> 32), n - 1);
+                x = ((unsigned long long)xhi << 32) | xlo;
+                if (rdlane(rnv, n - 1)) {
+                    bad |= p >= nw;
+                    ++p;
+                    if (__builtin_expect(p - p0 >= 64, 0)) {
+                        p0 = p;
+                        wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+                    }
+                    wnext = p < nw ? rdlane(wbuf, p - p0) : 0u;
+                }
+                int v = lo + n - 1;
+                if (__builtin_expect(v == len - 2, 0)) {   // escape: value coded in 4-bit bypass chunks
+                    uint32_t cc = get_bits(4), nb = cc;
+                    while (cc == 15u && nb <= 8) { cc = get_bits(4); nb += cc; }
+                    if (nb > 8) { bad |= 4; nb = 0; }
+                    uint32_t rawb = 0;
+                    for (uint32_t jj = 0; jj < nb; ++jj) rawb |= get_bits(4) << (jj * 4);
+                    v = (int)(rawb >> 1);
+                    v = (rawb & 1) ? -v - 1 : v + len - 2;
+                }
+                symv = lane == i ? v : symv;
+            }
+        }
+        if (lane < cnt)
+            a.yq[(long)row * a.ldy + i0 + lane] = (float)(symv + off_l) + a.ksi[(long)row * a.ldk + Mlat + i0 + lane];
     }
     if (lane == 0) {
         a.state_x[img] = x;
@@ -630,7 +796,11 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * RANS_WPB + (threadIdx.x >> 6);
+#ifdef LBIC_RANS_V1
     if (row < a.rows) rans_row(a, lcdf, lcdf + a.total16, row, lane);
+#else
+    if (row < a.rows) rans_row_spec(a, lcdf, lcdf + a.total16, row, lane);
+#endif
     stamp_end(a.ts);
 }
 
@@ -670,6 +840,29 @@ __global__ void k_copy_interior(const float* __restrict__ zpad, float* __restric
         const long src = ((long)(img * (Hb + 2) + v + 2) * (Wb + 4) + h + 2) * Cx + c;
         *reinterpret_cast<f4*>(zout + e) = *reinterpret_cast<const f4*>(zpad + src);
     }
+}
+
+__global__ void k_fill_interior(const float* __restrict__ zin, float* __restrict__ zpad, int n_img, int Hb, int Wb,
+                                int Cx) {
+    const long total = (long)n_img * Hb * Wb * Cx / 4;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long e = i * 4;
+        const int c = (int)(e % Cx);
+        long t = e / Cx;
+        const int h = (int)(t % Wb);
+        t /= Wb;
+        const int v = (int)(t % Hb);
+        const int img = (int)(t / Hb);
+        const long dst = ((long)(img * (Hb + 2) + v + 2) * (Wb + 4) + h + 2) * Cx + c;
+        *reinterpret_cast<f4*>(zpad + dst) = *reinterpret_cast<const f4*>(zin + e);
+    }
+}
+
+int launch_fill_interior(const float* zin, float* zpad, int n_img, int Hb, int Wb, int Cx, hipStream_t s) {
+    const long total = (long)n_img * Hb * Wb * Cx / 4;
+    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill_interior, dim3(blocks), dim3(256), 0, s, zin, zpad, n_img, Hb, Wb, Cx);
+    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "fill launch failed");
 }
 
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s) {

@@ -102,6 +102,10 @@ int main(int argc, char** argv) {
     float* yq; (void)hipMalloc(&yq, sizeof(float) * n_img * M * steps);
     a.blocks = (const int4*)up(blocks.data(), blocks.size() * sizeof(int4));
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+#ifdef LBIC_RANS_STAMPS
+    unsigned long long* dbg; (void)hipMalloc(&dbg, 8 * 4 * n_img); (void)hipMemset(dbg, 0, 8 * 4 * n_img);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rdbg), &dbg, sizeof(dbg));
+#endif
     (void)hipEventRecord(e0, nullptr);
     for (int st = 0; st < steps; ++st) {
         a.idx = idx_d + (size_t)st * n_img * M;
@@ -118,6 +122,13 @@ int main(int argc, char** argv) {
         for (int im = 0; im < n_img; ++im)
             for (int k = 0; k < M; ++k)
                 bad += (int)out[((size_t)st * n_img + im) * M + k] != sym[((size_t)im * steps + st) * M + k];
+#ifdef LBIC_RANS_STAMPS
+    { std::vector<unsigned long long> d(4 * n_img); (void)hipMemcpy(d.data(), dbg, 8 * 4 * n_img, hipMemcpyDeviceToHost);
+      double t[4] = {0, 0, 0, 0};
+      for (int im = 0; im < n_img; ++im) for (int k = 0; k < 4; ++k) t[k] += d[im * 4 + k] / (double)M / n_img;
+      printf("per-symbol cycles (last step, mean over images, incl ~40/stamp): idx->LUT %.0f, window %.0f, state %.0f, tail %.0f\n",
+             t[0], t[1], t[2], t[3]); }
+#endif
     printf("rans decode: %d images x %d symbols: %.2f us/step, %.0f ns/symbol, mismatches %ld\n", n_img, M,
            ms * 1e3 / steps, ms * 1e6 / steps / M, bad);
     return 0;

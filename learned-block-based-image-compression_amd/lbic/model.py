@@ -201,6 +201,26 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
+    def forward(self, zhat: torch.Tensor, x: torch.Tensor):
+        """BlockBasedImgCompLossyNetv4.forward(zhat, x) (net:90-106, inherited by v9) in eval semantics:
+        teacher forced on the given reconstruction, full-frame convolutions.  zhat, x: [n, 3B^2, Hb, Wb]
+        (block->channel layout of arrange_block_pixels_to_channel_dim).  Returns (xhat [n, 3B^2, Hb, Wb],
+        self_information [n, M, Hb, Wb] = -log2 p), like the reference; xhat is not clamped."""
+        self._check_ready()
+        if zhat.shape != x.shape or zhat.dim() != 4 or zhat.shape[1] != self.arch.cx:
+            raise ValueError(f"forward expects zhat, x of shape [n, {self.arch.cx}, Hb, Wb]")
+        n, _, Hb, Wb = x.shape
+        xb = x.to(self.device, torch.float32).permute(0, 2, 3, 1).contiguous()
+        zb = zhat.to(self.device, torch.float32).permute(0, 2, 3, 1).contiguous()
+        xhat = torch.empty_like(xb)
+        info = torch.empty((n, Hb, Wb, self.arch.M), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(_lib.lib().lbc_forward(self._h, _lib.ptr(xb), _lib.ptr(zb), n, Hb, Wb, _lib.ptr(xhat),
+                                          _lib.ptr(info), ctypes.c_void_p(stream)))
+        return xhat.permute(0, 3, 1, 2), info.permute(0, 3, 1, 2)
+
+    __call__ = forward
+
     def profile_begin(self, sample_every: int):
         """Sample every n-th step's kernels with HIP events (lbc_profile_begin)."""
         _lib.check(_lib.lib().lbc_profile_begin(self._h, int(sample_every)))

@@ -268,6 +268,41 @@ class OracleNet:
         return self._lin("prtr_inverse3.5", [h])
 
 
+    def forward_frame(self, zhat, x):
+        """forward(zhat, x) (net:90-106, inherited by v9; eval mode): teacher forced on a given zhat with the
+        full-frame 'same' convolutions of the nn.Sequential layers.  Differs from the closed loop only for
+        KS[1] = 3, where the 3x3 'B' layer of get_meanscale zero-pads the layer-0 MAP at the frame border
+        (the closed loop evaluates layer 0 on the zero-padded zhat there).  zhat, x: [Hb, Wb, C].
+        Returns xhat [Hb, Wb, C] (not clamped) and self-information -log2 p [Hb, Wb, M]."""
+        a = self.a
+        Hb, Wb, C = zhat.shape
+        zp = np.zeros((Hb + 2, Wb + 2, C), F32)
+        zp[1:-1, 1:-1] = zhat
+        l0 = np.zeros((Hb, Wb, self.conv["get_meanscale.0"][1].shape[0]), F32)
+        for v in range(Hb):
+            for h in range(Wb):
+                l0[v, h] = _leaky(self._lin("get_meanscale.0", self._taps(zp, (v + 1, h + 1), TAPS_A3)))
+        l0p = np.zeros((Hb + 2, Wb + 2, l0.shape[2]), F32)
+        l0p[1:-1, 1:-1] = l0
+        xhat = np.zeros_like(zhat)
+        info = np.zeros((Hb, Wb, a.M), F32)
+        for v in range(Hb):
+            for h in range(Wb):
+                if a.KS[1] == 3:
+                    l1 = _leaky(self._lin("get_meanscale.2", self._taps(l0p, (v + 1, h + 1), TAPS_B3)))
+                else:
+                    l1 = _leaky(self._lin("get_meanscale.2", [l0[v, h]]))
+                l2 = _leaky(self._lin("get_meanscale.4", [l1]))
+                ksi = self._lin("get_meanscale.6", [l2])
+                scales, means = ksi[:a.M], ksi[a.M:]
+                win = zp[v:v + 3, h:h + 3]
+                y = self.fwd(win, x[v, h])
+                yq = (np.rint((y - means).astype(F32)) + means).astype(F32)   # quantize(..., "dequantize")
+                info[v, h] = likelihood_bits(yq, scales, means)
+                xhat[v, h] = self.inv(win, yq)
+        return xhat, info
+
+
 class OracleCodec:
     """compress()/decompress() of the reference, one image, raster closed loop."""
 

@@ -14,6 +14,8 @@ Fixtures written:
   loop_<name>.npz        reference compress() closed loop: x (block-major), symbols, indexes, zhat, and
                          decompress() run teacher-forced on the recorded symbols (zhat_dec)
   stages_b8_lowrate.npz  per-stage activations of compress_blk for a few blocks of the 2-row B8 frame
+  forward_<name>.npz     the reference's teacher-forced forward(zhat, x) (net:90-106, eval mode) on a given
+                         zhat: xhat and self-information -log2 p, full-frame conv semantics
 """
 from __future__ import annotations
 
@@ -67,7 +69,7 @@ class Recorder:
         gc.build_indexes = self.build_indexes
 
     def quantize(self, inputs, mode, means=None):
-        if mode == "symbols":
+        if mode in ("symbols", "dequantize"):
             self.d.append((inputs - means).detach().double().flatten().numpy())
         return self._q(inputs, mode, means)
 
@@ -206,10 +208,51 @@ def gen_stages(model, x, zhat, arch, out):
     print("stages written:", out)
 
 
+FORWARDS = {
+    "tiny_ks3111": (Arch(4, (3, 1, 1, 1), 64, 16), 32, 32, 700),
+    "tiny_ks3311": (Arch(4, (3, 3, 1, 1), 64, 16), 32, 32, 800),
+}
+
+
+def gen_forward(name, arch, H, W, seed0):
+    """forward(zhat, x) of the reference (inherited from v4, net:90-106) in eval mode: zhat is an arbitrary
+    reconstruction (uniform noise in [-1/2, 1/2]), tie-screened on y - mu like the closed loops."""
+    sd = synth_state_dict(arch, WEIGHT_SEED)
+    model, net = refshim.make_model(arch, sd)
+    model.update(force=True)
+    seed = seed0
+    while True:
+        img = synth_image(seed, H, W)
+        x = to_blocks(img, arch.B)
+        zhat = torch.from_numpy(np.random.default_rng(seed + 10000).uniform(-0.5, 0.5, tuple(x.shape))
+                                .astype(np.float32))
+        rec = Recorder(model.conditional_gaussian_model)
+        with torch.no_grad():
+            xhat, self_info = model(zhat, x)
+        d = np.concatenate(rec.d)
+        margin = np.abs(np.abs(d - np.floor(d)) - 0.5).min()
+        model.conditional_gaussian_model.quantize = rec._q
+        model.conditional_gaussian_model.build_indexes = rec._b
+        print(f"forward {name}: seed {seed} margin {margin:.2e}", flush=True)
+        if margin > TIE_EPS:
+            break
+        seed += 1
+        assert seed < seed0 + 400, "no tie-free seed found"
+    bm = lambda t: t[0].permute(1, 2, 0).contiguous().numpy()     # [C, Hb, Wb] -> [Hb, Wb, C]
+    np.savez_compressed(
+        os.path.join(HERE, f"forward_{name}.npz"),
+        B=arch.B, KS=np.array(arch.KS), N=arch.N, M=arch.M, weight_seed=WEIGHT_SEED, image_seed=seed,
+        x=bm(x), zhat=bm(zhat), xhat=bm(xhat), self_info=bm(self_info))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     gen_cdf(os.path.join(HERE, "cdf_pmf.npz"))
     only = sys.argv[1:]
+    for name, (arch, H, W, s0) in FORWARDS.items():
+        if only and ("forward_" + name) not in only:
+            continue
+        gen_forward(name, arch, H, W, s0)
     for name, (arch, H, W, s0) in LOOPS.items():
         if only and name not in only:
             continue

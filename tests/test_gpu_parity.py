@@ -183,3 +183,44 @@ def test_substream_format_roundtrip(name, tables):
     assert torch.equal(z, r["zhat"])
     if name == "b8_lowrate_2rows":
         assert np.array_equal(sym[0], g["symbols"])
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+def test_forward_matches_reference(name):
+    """forward(zhat, x) (net:90-106, eval) on the GPU against the reference's own output on the same given
+    zhat: xhat within 1e-5, self-information within 1e-4 relative."""
+    g = load_golden("forward_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    to = lambda a: torch.from_numpy(a).permute(2, 0, 1)[None].cuda()          # [Hb, Wb, C] -> [1, C, Hb, Wb]
+    xhat, info = m.forward(to(g["zhat"]), to(g["x"]))
+    assert xhat.shape == (1, arch.cx, 8, 8) and info.shape == (1, arch.M, 8, 8)
+    xhat = xhat[0].permute(1, 2, 0).cpu().numpy()
+    info = info[0].permute(1, 2, 0).cpu().numpy()
+    assert np.abs(xhat - g["xhat"]).max() < 1e-5
+    assert (np.abs(info - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "b8_lowrate_2rows", "tiny_ks3311"])
+def test_forward_on_closed_loop_reconstruction(name):
+    """Teacher forcing on the closed loop's own zhat reproduces the closed loop: clamp(xhat) = zhat and the
+    self-information equals the encoder's bits, bit for bit (same kernels, same slice order).  KS3311:
+    the blocks whose context window lies inside the frame (the border differs by design: forward()
+    zero-pads the layer-0 map, compress() evaluates it on the zero-padded zhat)."""
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    x = torch.from_numpy(g["x"])[None].cuda()
+    r = m.compress_batch(x, want_bits=True)
+    Hb, Wb = g["x"].shape[:2]
+    xhat, info = m.forward(r["zhat"].permute(0, 3, 1, 2), x.permute(0, 3, 1, 2))
+    zf = torch.clamp(xhat, -0.5, 0.5).permute(0, 2, 3, 1)
+    bits = r["bits"].view(1, Hb, Wb, arch.M)
+    inf = info.permute(0, 2, 3, 1)
+    if arch.KS[1] == 3:
+        sl = (slice(None), slice(1, Hb), slice(1, Wb - 1))
+        zf, z0, bits, inf = zf[sl], r["zhat"][sl], bits[sl], inf[sl]
+    else:
+        z0 = r["zhat"]
+    assert torch.equal(zf, z0)
+    assert torch.equal(inf, bits)

@@ -112,3 +112,15 @@ def test_closed_loop_matches_reference(name):
     if name in ("tiny_ks3111", "tiny_ks3311"):
         zdec = codec.decompress(out["bytes"], *g["x"].shape[:2])
         assert np.array_equal(zdec, out["zhat"])
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+def test_oracle_forward_matches_reference(name):
+    """The oracle's teacher-forced full-frame forward (net:90-106) against the reference's forward() fixture:
+    xhat within 1e-5, self-information within 1e-4 relative (fp32 erfc)."""
+    g = load_golden("forward_" + name)
+    arch = golden_arch(g)
+    net = O.OracleNet(arch, synth_state_dict(arch, int(g["weight_seed"])))
+    xhat, info = net.forward_frame(g["zhat"], g["x"])
+    assert np.abs(xhat - g["xhat"]).max() < 1e-5
+    assert (np.abs(info - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
