@@ -554,21 +554,28 @@ __device__ unsigned long long* g_rdbg;
 #define RSTAMP(var)
 #define RACC(k, d)
 #endif
-__device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
-                                         int lane) {
-    const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
-    const int4 blk = blocks[row];
-    // stream / state of this row: the image's (reference format) or the block row's (sub-stream format)
-    const int img = __builtin_amdgcn_readfirstlane(a.streams_per_img > 1 ? blk.x * a.streams_per_img + blk.y : blk.x);
+// Called by every wave of the workgroup (rows past a.rows only help fill the LDS tables): the wave's
+// stream state is requested first, the workgroup then copies the CDF tables + LUT into LDS while those
+// loads are in flight, and only the stream window (which depends on them) waits for the barrier.
+__device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int row_in, int lane) {
+    const bool valid = row_in < a.rows;
+    const int row = valid ? row_in : a.rows - 1;
+    // stream / state of this row: the image's (reference format: row = image) or the block row's
+    // (sub-stream format, via the block list)
+    int img = row;
+    if (a.streams_per_img > 1) {
+        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
+        const int4 blk = blocks[row];
+        img = blk.x * a.streams_per_img + blk.y;
+    }
+    img = __builtin_amdgcn_readfirstlane(img);
     const int Mlat = a.Mlat;
     // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
     const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
-    unsigned long long x = uni64(a.state_x[img]);
-    int p = __builtin_amdgcn_readfirstlane(a.state_ptr[img]);
-    const uint32_t* w = a.words + a.word_base[img];
-    const int nw = __builtin_amdgcn_readfirstlane(a.word_count[img]);
-    int p0 = p;
-    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+    const unsigned long long x_in = a.state_x[img];
+    const int p_in = a.state_ptr[img];
+    const long long wb = a.word_base[img];
+    const int nw_in = a.word_count[img];
     int idxr[4], symr[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -576,6 +583,21 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
         idxr[kb] = i < Mlat ? a.idx[(long)row * Mlat + i] : 0;
         symr[kb] = 0;
     }
+    {   // CDF tables + start-index LUT (both built on the host, contiguous in cdf16)
+        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (int i = threadIdx.x; i < (a.total16 + 64 * 256) / 8; i += blockDim.x) dst[i] = src[i];
+    }
+    unsigned long long x = uni64(x_in);
+    int p = __builtin_amdgcn_readfirstlane(p_in);
+    const uint32_t* w = a.words + wb;
+    const int nw = __builtin_amdgcn_readfirstlane(nw_in);
+    int p0 = p;
+    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+    __syncthreads();
+    if (!valid) return;
+    const uint16_t* lcdf = lds;
+    const uint16_t* llut = lds + a.total16;
     int bad = 0;
 #ifdef LBIC_RANS_STAMPS
     unsigned long long acc[4] = {0, 0, 0, 0};
@@ -665,142 +687,12 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, const uint16_t* lcdf
     }
 }
 
-// Speculative form of rans_row (same stream semantics, same outputs).  Per symbol every lane j of the
-// CDF window [lo, lo+64) computes the state that WOULD follow if the symbol were lo+j, renormalisation
-// included, in vector registers while the ballot finds the actual symbol; the state then comes back
-// with three v_readlane.  The start-index LUT rows of RANS_CH symbols sit in registers (one bucket
-// lookup = two v_readlane), and the per-symbol table data (base, length) is read from lane-distributed
-// registers off the critical path.  Dependent chain per symbol: bucket -> one LDS window read ->
-// compare/ballot (beside the speculative state) -> readlane.
-constexpr int RANS_CH = 32;
-
-__device__ __forceinline__ void rans_row_spec(const RansArgs& a, const uint16_t* lcdf, const uint16_t* llut, int row,
-                                              int lane) {
-    int img = row;
-    if (a.streams_per_img > 1) {
-        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
-        const int4 blk = blocks[row];
-        img = blk.x * a.streams_per_img + blk.y;
-    }
-    img = __builtin_amdgcn_readfirstlane(img);
-    const int Mlat = a.Mlat;
-    const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
-    unsigned long long x = uni64(a.state_x[img]);
-    int p = __builtin_amdgcn_readfirstlane(a.state_ptr[img]);
-    const uint32_t* w = a.words + a.word_base[img];
-    const int nw = __builtin_amdgcn_readfirstlane(a.word_count[img]);
-    int p0 = p;
-    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-    uint32_t wnext = rdlane(wbuf, 0);
-    int bad = 0;
-    auto get_bits = [&](int nb) -> uint32_t {      // bypass chunks (escapes only)
-        const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
-        x >>= nb;
-        if (x < (1ull << 31)) {
-            bad |= p >= nw;
-            x = (x << 32) | wnext;
-            ++p;
-            if (p - p0 >= 64) {
-                p0 = p;
-                wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-            }
-            wnext = p < nw ? rdlane(wbuf, p - p0) : 0u;
-        }
-        x = uni64(x);
-        return v;
-    };
-    for (int i0 = 0; i0 < Mlat; i0 += RANS_CH) {
-        const int cnt = min(RANS_CH, Mlat - i0);
-        const int ci_l = lane < cnt ? (a.idx[(long)row * Mlat + i0 + lane] & 63) : 0;
-        // lane i: table data of symbol i0+i
-        const int base_l = __shfl(t_base, ci_l), len_l = __shfl(t_len, ci_l), off_l = __shfl(t_off, ci_l);
-        uint32_t L0[RANS_CH], L1[RANS_CH];
-#pragma unroll
-        for (int i = 0; i < RANS_CH; ++i) {
-            const int ci = __builtin_amdgcn_readlane(ci_l, i);
-            const uint2 v = *reinterpret_cast<const uint2*>(llut + ci * 256 + lane * 4);
-            L0[i] = v.x;
-            L1[i] = v.y;
-        }
-        int symv = 0;
-#pragma unroll
-        for (int i = 0; i < RANS_CH; ++i) {
-            if (i < cnt) {
-                const int base = __builtin_amdgcn_readlane(base_l, i);
-                const int len = __builtin_amdgcn_readlane(len_l, i);
-                const uint32_t cum = (uint32_t)x & 0xffffu;
-                const unsigned long long xq = x >> 16;
-                const uint32_t e = cum >> 8;
-                const uint32_t w0 = rdlane(L0[i], e >> 2), w1 = rdlane(L1[i], e >> 2);
-                const uint32_t ww = (e & 2) ? w1 : w0;
-                int lo = (int)((ww >> ((e & 1) * 16)) & 0xffffu);
-                int n;
-                unsigned long long xr;
-                uint32_t rnv;
-                for (;;) {
-                    const int j = lo + lane;
-                    const uint32_t r0 = lcdf[base + j], r1 = lcdf[base + j + 1];
-                    const uint32_t c0 = j < len - 1 ? r0 : 65536u;
-                    const uint32_t c1 = j + 1 < len - 1 ? r1 : 65536u;
-                    n = __popcll(__ballot(c0 <= cum));
-                    // speculative next state of lane j's symbol (only lane n-1's is used)
-                    const unsigned long long xn = (unsigned long long)(c1 - c0) * xq + (cum - c0);
-                    const bool rn = xn < (1ull << 31);
-                    xr = rn ? ((xn << 32) | wnext) : xn;
-                    rnv = rn ? 1u : 0u;
-                    if (__builtin_expect(n < 64, 1)) break;
-                    lo += 64;      // interval beyond this window (distribution tails)
-                }
-                const uint32_t xlo = rdlane((uint32_t)xr, n - 1), xhi = rdlane((uint32_t)(xr >> 32), n - 1);
-                x = ((unsigned long long)xhi << 32) | xlo;
-                if (rdlane(rnv, n - 1)) {
-                    bad |= p >= nw;
-                    ++p;
-                    if (__builtin_expect(p - p0 >= 64, 0)) {
-                        p0 = p;
-                        wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-                    }
-                    wnext = p < nw ? rdlane(wbuf, p - p0) : 0u;
-                }
-                int v = lo + n - 1;
-                if (__builtin_expect(v == len - 2, 0)) {   // escape: value coded in 4-bit bypass chunks
-                    uint32_t cc = get_bits(4), nb = cc;
-                    while (cc == 15u && nb <= 8) { cc = get_bits(4); nb += cc; }
-                    if (nb > 8) { bad |= 4; nb = 0; }
-                    uint32_t rawb = 0;
-                    for (uint32_t jj = 0; jj < nb; ++jj) rawb |= get_bits(4) << (jj * 4);
-                    v = (int)(rawb >> 1);
-                    v = (rawb & 1) ? -v - 1 : v + len - 2;
-                }
-                symv = lane == i ? v : symv;
-            }
-        }
-        if (lane < cnt)
-            a.yq[(long)row * a.ldy + i0 + lane] = (float)(symv + off_l) + a.ksi[(long)row * a.ldk + Mlat + i0 + lane];
-    }
-    if (lane == 0) {
-        a.state_x[img] = x;
-        a.state_ptr[img] = p;
-        if (bad) a.status[img] = bad;
-    }
-}
-
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
     stamp_start(a.ts);
-    {   // CDF tables + start-index LUT (both built on the host, contiguous in cdf16)
-        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
-        uint4* dst = reinterpret_cast<uint4*>(lcdf);
-        for (int i = threadIdx.x; i < (a.total16 + 64 * 256) / 8; i += blockDim.x) dst[i] = src[i];
-    }
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * RANS_WPB + (threadIdx.x >> 6);
-#ifdef LBIC_RANS_V1
-    if (row < a.rows) rans_row(a, lcdf, lcdf + a.total16, row, lane);
-#else
-    if (row < a.rows) rans_row_spec(a, lcdf, lcdf + a.total16, row, lane);
-#endif
+    rans_row(a, lcdf, row, lane);
     stamp_end(a.ts);
 }
 
