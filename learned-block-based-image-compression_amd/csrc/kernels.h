@@ -63,7 +63,6 @@ struct GemmArgs {
     float* bits;
     int HW;
     Geo geo;
-    int xcd_map;             // experiment: column tile t on XCD t % 8
     int zero_oob;            // EPI_LEAKY: rows whose context position lies outside the frame are written as 0
                              // (forward()'s zero padding of the layer-0 map, KS[1] = 3)
 };

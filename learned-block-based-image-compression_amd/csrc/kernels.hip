@@ -419,11 +419,7 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int nt = blockIdx.x;
-    if (g.xcd_map) {      // column tile t runs on XCD t % 8 (assumes round-robin dispatch; experiment only)
-        nt = xcc_id() + 8 * (blockIdx.x >> 3);
-        if (nt * 16 >= g.N) return;
-    }
+    const int nt = blockIdx.x;
     const int n0 = nt * 16, m0 = blockIdx.y * 16;
     stamp_start(g.ts);
     PHASE(0);
@@ -507,7 +503,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     }
     if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
-        dim3 grid(g.xcd_map ? ((g.N + 127) / 128) * 8 : (g.N + 15) / 16, (g.M + 15) / 16);
+        dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
         switch ((g.K >> 4) / KSPLIT) {
 #define LBIC_L(L) case L: hipLaunchKernelGGL(k_gemm_s<L>, grid, dim3(512), 0, s, g); break;
             LBIC_L(0) LBIC_L(1) LBIC_L(2) LBIC_L(3) LBIC_L(4) LBIC_L(5) LBIC_L(6)

@@ -13,8 +13,7 @@ int set_error(int code, const std::string& msg) { fprintf(stderr, "%s\n", msg.c_
 using namespace lbic;
 
 int main(int argc, char** argv) {
-    const int xcd = argc > 1 ? atoi(argv[1]) : 0;
-    const int hot = argc > 2 ? atoi(argv[2]) : 0;   // 1: every WG reads the same few KB (L1/L2-hot)
+    const int hot = argc > 1 ? atoi(argv[1]) : 0;   // 1: every WG reads the same few KB (L1/L2-hot)
     const int M = 32;
     struct L { int K, N, epi; const char* name; };
     const L layers[] = {{768, 1152, EPI_LEAKY, "ctx0"}, {1152, 960, EPI_LEAKY, "ctx1"}, {960, 768, EPI_LEAKY, "ctx2"},
@@ -45,7 +44,6 @@ int main(int argc, char** argv) {
         g.blocks = blocks; g.W = W; g.NB16 = (g.N + 15) / 16; g.bias = bias; g.epi = layers[i].epi;
         g.out = act[(i + 1) & 1]; g.ldo = 1152; g.gx = act[i & 1]; g.ldx = 1152;
         g.ctr_stride = i;    // phase slot
-        g.xcd_map = xcd;
         if (hot) { g.NB16 = 0; g.seg[0].ld = 0; }
         gs[i] = g;
     }
@@ -79,7 +77,7 @@ int main(int argc, char** argv) {
            "[3]->barrier [4]->epilogue done | span first start..last end\n");
     unsigned long long prev_end = 0;
     for (int i = 0; i < NL; ++i) {
-        const int nwg = (xcd ? ((gs[i].N + 127) / 128) * 8 : (gs[i].N + 15) / 16) * ((M + 15) / 16);
+        const int nwg = (((gs[i].N + 127) / 128) * 8) * ((M + 15) / 16);
         double acc[6] = {0, 0, 0, 0, 0, 0};
         unsigned long long t0 = ~0ull, t1 = 0;
         int live = 0;

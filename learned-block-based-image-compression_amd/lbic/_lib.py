@@ -10,6 +10,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblbic.so")
+if os.environ.get("LBIC_LIB_VARIANT"):      # A/B experiments: lbic/liblbic_<variant>.so built from another revision
+    LIB_PATH = os.path.join(HERE, f"liblbic_{os.environ['LBIC_LIB_VARIANT']}.so")
 
 LBC_E_NOT_UPDATED = -4
 
