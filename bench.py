@@ -5,7 +5,10 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU.  One step = the reference's timed region of eval_model
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
-GPU rANS decode).  Inputs are resident in HBM when the timed region starts.  Weights are the seeded
+GPU rANS decode).  Steps are software-pipelined two deep (default): while batch k is decoded (latency-bound
+raster chain, few CUs busy) batch k+1 is compressed and entropy coded on another stream/handle; the timed
+region holds exactly `steps` compressions and `steps` decompressions (--serial: no overlap; a serial
+measurement is also reported under "serial_schedule").  Inputs are resident in HBM when the timed region starts.  Weights are the seeded
 synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
 checkpoints offline).
 
@@ -21,6 +24,7 @@ import re
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -85,6 +89,8 @@ def main():
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
+    ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
     ap.add_argument("--substream-steps", type=int, default=2,
                     help="extra steps in the opt-in per-row sub-stream format, reported apart (0 = skip)")
     args = ap.parse_args()
@@ -111,9 +117,17 @@ def main():
     Hb, Wb = H // B, W // B
     cfg = types.SimpleNamespace(block_size=B, KS=list(KS), N=N, M=M, gpu_device=local)
     sd = synth_state_dict(arch, 1337)
-    model = BlockBasedImgCompLossyNetv9(cfg, device=dev)
-    model.load_state_dict(sd)
-    model.update(force=True)
+
+    def make_model():
+        m = BlockBasedImgCompLossyNetv9(cfg, device=dev)
+        m.load_state_dict(sd)
+        m.update(force=True)
+        return m
+
+    # two codec handles (own workspaces and reconstruction buffers): the encoder side and the decoder side
+    # of the two-stage pipeline; the decoder gets its own HIP stream
+    enc_model, dec_model = make_model(), make_model()
+    s_enc, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
     n = args.batch
     frames = np.stack([image_to_blocks(np.random.default_rng(rank * n + k).integers(0, 256, (3, H, W), dtype=np.uint8)
@@ -121,78 +135,113 @@ def main():
     xb = torch.from_numpy(frames).to(dev)
     del frames
 
-    phase = dict(encode=0.0, entropy=0.0, decode=0.0)
-
-    def step(record=False, fmt="reference"):
-        t0 = time.perf_counter()
-        r = model.compress_batch(xb)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        streams = model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
-        t2 = time.perf_counter()
-        z = model.decompress_batch(streams, Hb, Wb, fmt=fmt)
-        torch.cuda.synchronize(dev)
-        t3 = time.perf_counter()
-        if record:
-            phase["encode"] += t1 - t0
-            phase["entropy"] += t2 - t1
-            phase["decode"] += t3 - t2
-        return r, streams, z
-
-    # sampling is part of the captured graphs: enable it before the warmup builds them
-    model.profile_begin(args.sample_every)
-    for i in range(args.warmup):
-        step()
-        log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
-
     def barrier():
         if dist:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
-    model.profile_begin(args.sample_every)     # same period: keeps the graphs, restarts launch counts
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        r, streams, z = step(record=True)
-        log(f"[rank {rank}] step {i + 1}/{args.steps}: {time.perf_counter() - t0:.2f} s")
-    barrier()
-    dt = time.perf_counter() - t0
-    kstats = model.profile_end()
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    def max_over_ranks(v):
+        if dist:
+            t = torch.tensor([v], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            v = float(t.item())
+        return v
+
+    def encode_side(fmt, ph):
+        """compress (GPU) + host rANS of one batch on the encoder stream -> (result, streams)"""
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_enc):
+            r = enc_model.compress_batch(xb)
+            s_enc.synchronize()
+            t1 = time.perf_counter()
+            st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
+        ph["encode"] += t1 - t0
+        ph["entropy"] += time.perf_counter() - t1
+        return r, st
+
+    def decode_side(st, fmt, ph, out):
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_dec):
+            z = dec_model.decompress_batch(st, Hb, Wb, fmt=fmt)
+            s_dec.synchronize()
+        ph["decode"] += time.perf_counter() - t0
+        out.append(z)
+
+    def collect_stats():
+        ks = {}
+        for m_ in (enc_model, dec_model):           # merge the two handles' per-kernel records
+            for name, st_ in (m_.profile_end() or {}).items():
+                acc = ks.setdefault(name, dict(launches=0, total_launches=0, total_ms=0.0, flops=0.0, bytes=0.0))
+                for k_ in acc:
+                    acc[k_] += st_[k_]
+        return ks
+
+    def run(fmt, steps, warmup, pipelined, label, prof=False):
+        """`steps` timed batches.  Pipelined: step k decodes batch k-1 (decoder stream, helper thread; ctypes
+        drops the GIL) while batch k is compressed and entropy coded (encoder stream, this thread), so the
+        timed region holds exactly `steps` encodes and `steps` decodes; the pipeline is primed with one
+        encode and drained with one decode outside it.  Serial: encode, entropy, decode one after another."""
+        ph = dict(encode=0.0, entropy=0.0, decode=0.0)
+        scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
+        for i in range(warmup):
+            r, st = encode_side(fmt, scratch)
+            decode_side(st, fmt, scratch, [])
+            log(f"[rank {rank}] {label} warmup {i + 1}/{warmup} done")
+        prev = encode_side(fmt, scratch) if pipelined else None     # prime: batch 0 encoded
+        last = None
+        if prof:      # launch counts cover the timed region only (same sampling period: graphs are kept)
+            for m_ in (enc_model, dec_model):
+                m_.profile_begin(args.sample_every)
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if pipelined:
+                out = []
+                th = threading.Thread(target=decode_side, args=(prev[1], fmt, ph, out))
+                th.start()
+                cur = encode_side(fmt, ph)
+                th.join()
+                last = (prev[0], prev[1], out[0])
+                prev = cur
+            else:
+                r, st = encode_side(fmt, ph)
+                out = []
+                decode_side(st, fmt, ph, out)
+                last = (r, st, out[0])
+            log(f"[rank {rank}] {label} step {i + 1}/{steps}: {time.perf_counter() - t0:.2f} s")
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        ks = collect_stats() if prof else None
+        if pipelined:                                               # drain (outside the timed region)
+            decode_side(prev[1], fmt, scratch, [])
+        return dt, ph, last, ks
+
+    # sampling is part of the captured graphs: enable it before the warmup builds them
+    for m_ in (enc_model, dec_model):
+        m_.profile_begin(args.sample_every)
+    pipelined = not args.serial
+    run("reference", 0, args.warmup, False, "warmup")
+    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, pipelined, "reference", prof=True)
+    serial = None
+    if pipelined and args.serial_steps > 0:     # the same batches without the overlap, for reference
+        dts, phs, _, _ = run("reference", args.serial_steps, 0, False, "serial")
+        serial = dict(value=round(world * n * H * W / (dts / args.serial_steps) / 1e6, 4),
+                      ms_per_step=round(dts / args.serial_steps * 1e3, 2), steps=args.serial_steps,
+                      phases_ms_per_step={k: round(v / args.serial_steps * 1e3, 2) for k, v in phs.items()})
 
     # --- opt-in sub-stream format (SURVEY H1b): same encoder, one rANS stream per block row, wavefront
     #     decode.  Reported apart from the headline (which stays on the reference bitstream format).
     sub = None
     if args.substream_steps > 0:
-        for k in list(phase):
-            phase[k + "_ref"] = phase[k]
-            phase[k] = 0.0
-        step(fmt="rows")
-        barrier()
-        ts = time.perf_counter()
-        for i in range(args.substream_steps):
-            rs, ss, zs = step(record=True, fmt="rows")
-        barrier()
-        dts = time.perf_counter() - ts
-        if dist:
-            t = torch.tensor([dts], dtype=torch.float64, device=dev)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            dts = float(t.item())
-        sub_exact = bool(torch.equal(zs, rs["zhat"]))
+        run("rows", 0, 1, False, "rows warmup")
+        dts, phs, (rs, ss, zs), _ = run("rows", args.substream_steps, 0, pipelined, "rows")
         sub = dict(value=round(world * n * H * W / (dts / args.substream_steps) / 1e6, 4),
                    ms_per_step=round(dts / args.substream_steps * 1e3, 2), steps=args.substream_steps,
                    bpp=round(float(np.mean([len(b) * 8.0 / (H * W) for b in ss])), 5),
-                   enc_dec_bit_exact_rank0=sub_exact,
-                   phases_ms_per_step={k: round(phase[k] / args.substream_steps * 1e3, 2) for k in
-                                       ("encode", "entropy", "decode")})
-        for k in ("encode", "entropy", "decode"):
-            phase[k] = phase.pop(k + "_ref")
+                   enc_dec_bit_exact_rank0=bool(torch.equal(zs, rs["zhat"])),
+                   phases_ms_per_step={k: round(v / args.substream_steps * 1e3, 2) for k, v in phs.items()})
 
-    # --- quality / consistency of the last step (outside the timed region)
+    # --- quality / consistency of the last decoded batch (outside the timed region)
     bit_exact = bool(torch.equal(z, r["zhat"]))
     sse = ((z - xb) ** 2).double().sum(dim=(1, 2, 3))
     rec = torch.stack([torch.tensor([float(len(s)) for s in streams], dtype=torch.float64, device=dev), sse,
@@ -269,13 +318,17 @@ def main():
         "config": {"workload": f"{args.config} N{N}M{M}, batch of {n} synthetic {H}x{W} frames per GPU, "
                                "encode+decode in the reference bitstream format (one raster rANS stream per image)",
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
-                   "global_batch": n * world},
+                   "global_batch": n * world,
+                   "schedule": "serial: encode, entropy, decode per batch" if args.serial else
+                   "two-stage pipeline: batch k+1 compress + host rANS overlaps batch k decode (2 codec handles, "
+                   "2 HIP streams); each timed step = one full encode and one full decode of a 32-frame batch"},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"bpp": round(bpp, 5), "psnr_db": round(psnr, 3), "enc_dec_bit_exact": bit_exact},
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
         "step_algorithmic_tflop": round(step_flops / 1e12, 3),
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
         "kernels": kernels,
+        "serial_schedule": serial,
         "substream_format": sub,
     }
     print(json.dumps(out), flush=True)
