@@ -32,7 +32,22 @@ Hb = Wb = H // 8
 xb = torch.from_numpy(np.stack([image_to_blocks(np.random.default_rng(k).integers(0, 256, (3, H, H), dtype=np.uint8)
                                                 .astype(np.float32) / 255 - 0.5, 8) for k in range(n)])).to(dev)
 PRIO = int(os.environ.get("PRIO", "0"))
+ENC_CUS = int(os.environ.get("ENC_CUS", "0"))
+
+
+def cu_masked_stream(n_cu):
+    """HIP stream restricted to the first n_cu compute units (hipExtStreamCreateWithCUMask)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    words = (ctypes.c_uint32 * 8)(*[0xffffffff if (w + 1) * 32 <= n_cu else ((1 << max(0, n_cu - w * 32)) - 1)
+                                   for w in range(8)])
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(8), words)
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(st.value, device=dev)
 sd_, se_ = (torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev, priority=0)) if PRIO else (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+if ENC_CUS:
+    se_ = cu_masked_stream(ENC_CUS)
 
 
 def enc(m):
