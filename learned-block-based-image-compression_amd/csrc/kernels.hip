@@ -693,6 +693,7 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
 }
 
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
+    if (a.rows <= 0) return LBC_OK;     // an empty wavefront step (e.g. odd steps of a one-column frame)
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
     if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 table must be padded to 16 bytes");
     const size_t lds = (size_t)(a.total16 + 64 * 256) * sizeof(uint16_t);

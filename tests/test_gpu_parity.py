@@ -224,3 +224,63 @@ def test_forward_on_closed_loop_reconstruction(name):
         z0 = r["zhat"]
     assert torch.equal(zf, z0)
     assert torch.equal(inf, bits)
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+@pytest.mark.parametrize("shape", [(1, 1), (1, 9), (7, 1), (3, 5)])
+def test_ragged_frames_roundtrip(name, shape):
+    """Frames of 1 block, one block row, one block column and a small odd rectangle: decode(encode) is bit
+    exact (reference and sub-stream formats), the streams equal the oracle coder's bytes, and teacher forcing
+    on the reconstruction reproduces it (KS3311: the blocks whose context lies inside the frame)."""
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    Hb, Wb = shape
+    rng = np.random.default_rng(Hb * 100 + Wb)
+    img = rng.integers(0, 256, (2, 3, Hb * arch.B, Wb * arch.B)).astype(np.float32) / 255 - 0.5
+    x = torch.from_numpy(np.stack([O.image_to_blocks(i, arch.B) for i in img])).cuda()
+    r = m.compress_batch(x, want_bits=True)
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    tabs = O.GaussianTables()
+    for k in range(2):
+        assert streams[k] == tabs.encode(r["symbols"][k].cpu().numpy(), r["indexes"][k].cpu().numpy())
+    assert torch.equal(m.decompress_batch(streams, Hb, Wb), r["zhat"])
+    rows = m.entropy_encode(r["symbols"], r["indexes"], fmt="rows", Hb=Hb, Wb=Wb)
+    assert torch.equal(m.decompress_batch(rows, Hb, Wb, fmt="rows"), r["zhat"])
+    xhat, info = m.forward(r["zhat"].permute(0, 3, 1, 2), x.permute(0, 3, 1, 2))
+    zf = torch.clamp(xhat, -0.5, 0.5).permute(0, 2, 3, 1)
+    inf = info.permute(0, 2, 3, 1)
+    bits = r["bits"].view(2, Hb, Wb, arch.M)
+    if arch.KS[1] == 3:
+        sl = (slice(None), slice(1, Hb), slice(1, Wb - 1))
+        zf, z0, inf, bits = zf[sl], r["zhat"][sl], inf[sl], bits[sl]
+    else:
+        z0 = r["zhat"]
+    assert torch.equal(zf, z0) and torch.equal(inf, bits)
+
+
+def test_bad_inputs_raise():
+    """Errors are loud: empty batches, truncated / corrupted streams, a wrong container, wrong shapes."""
+    g = load_golden("loop_tiny_ks3111")
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    x = torch.from_numpy(g["x"])[None].cuda()
+    r = m.compress_batch(x)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    Hb, Wb = g["x"].shape[:2]
+    with pytest.raises((ValueError, RuntimeError)):
+        m.compress_batch(x[:0])
+    with pytest.raises((ValueError, RuntimeError)):
+        m.decompress_batch([st[0][:8]], Hb, Wb)                    # truncated: the decoder runs out of words
+    with pytest.raises((ValueError, RuntimeError)):
+        m.decompress_batch([st[0][:5]], Hb, Wb)                    # not a whole number of 32-bit words
+    with pytest.raises((ValueError, RuntimeError)):
+        m.decompress_batch(st, Hb + 4, Wb)                         # more blocks than were coded
+    with pytest.raises((ValueError, RuntimeError)):
+        m.decompress_batch([b"XXXX" + st[0][4:]], Hb, Wb, fmt="rows")   # not an 'LBW1' container
+    with pytest.raises(ValueError):
+        m.compress_batch(x[..., :-1].contiguous())                 # wrong channel count
+    with pytest.raises(ValueError):
+        m.forward(x.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2)[:, :, :1])
+    # the handle still works afterwards
+    assert torch.equal(m.decompress_batch(st, Hb, Wb), r["zhat"])
