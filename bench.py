@@ -85,7 +85,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
-    ap.add_argument("--size", type=int, default=768)
+    ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
+    ap.add_argument("--height", type=int, default=0, help="frame height (default: --size)")
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
@@ -113,7 +114,8 @@ def main():
 
     B, KS, N, M = CONFIGS[args.config]
     arch = Arch(B, KS, N, M)
-    H = W = args.size
+    W = args.size
+    H = args.height or args.size
     Hb, Wb = H // B, W // B
     cfg = types.SimpleNamespace(block_size=B, KS=list(KS), N=N, M=M, gpu_device=local)
     sd = synth_state_dict(arch, 1337)
