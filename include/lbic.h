@@ -76,6 +76,14 @@ int lbc_set_entropy_tables(lbc_model *m, const float *scale_table, int n_tables,
 int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, float *zhat_dev,
                int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, void *stream);
 
+/* lbc_encode with flags.  LBC_ENC_FRAME_PAD: the context net's layer-0 map is zero outside the frame
+ * (forward()'s 'same' padding) instead of being evaluated on the zero-padded zhat (compress()): the closed
+ * loop of validate_recu_reco_fast (agents/blkbsdimgcomp_agent.py:491-520), which runs forward() on causal
+ * crops.  Differs from compress() only for KS[1] = 3; bits_dev then holds its self-information. */
+#define LBC_ENC_FRAME_PAD 1
+int lbc_encode_ex(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, float *zhat_dev,
+                  int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, int flags, void *stream);
+
 /* Teacher-forced forward pass, BlockBasedImgCompLossyNetv4.forward(zhat, x) inherited by v9
  * (graphs/models/BlockBasedImgCompLossy_net.py:90-106), eval mode: every block sees the GIVEN zhat
  * (no closed loop), with the full-frame 'same' convolutions of the reference's nn.Sequential layers.

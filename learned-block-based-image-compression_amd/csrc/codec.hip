@@ -717,9 +717,18 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
 
 int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, float* zhat_dev, int32_t* sym_dev,
                int32_t* idx_dev, float* bits_dev, void* stream) {
+    return lbc_encode_ex(m, x_dev, n_img, Hb, Wb, zhat_dev, sym_dev, idx_dev, bits_dev, 0, stream);
+}
+
+int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, float* zhat_dev, int32_t* sym_dev,
+                  int32_t* idx_dev, float* bits_dev, int flags, void* stream) {
+    if (flags & ~LBC_ENC_FRAME_PAD) return set_error(LBC_E_ARG, "unknown encode flags");
+    const bool frame_pad = (flags & LBC_ENC_FRAME_PAD) != 0;
     if (!m || !x_dev || !zhat_dev || !sym_dev || !idx_dev) return set_error(LBC_E_ARG, "null argument");
     if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
-    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    // the validation loop (frame_pad) uses forward()'s likelihood, not the CDFs: it runs before update()
+    // too (scale indexes are then not produced)
+    if (!m->tabs_set && !frame_pad) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
     if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
@@ -732,7 +741,7 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
     // the graph works on library-owned buffers only, so it survives new caller tensors
     const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->x_in.p, (long long)m->zpad.p,
                                         (long long)m->sym_buf.p, (long long)m->lane[0].ctx0.p,
-                                        (long long)m->table_dev.p, m->prof.sample_every};
+                                        (long long)m->table_dev.p, m->prof.sample_every, flags};
     if (!m->enc_exec || key != m->enc_key) {
         if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
         HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
@@ -745,7 +754,7 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
             m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
             GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), n_img, Hb, Wb);
-            if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap);
+            if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad);
             if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
                                     m->bits_buf.as<float>(), m->cap);
             if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
@@ -778,8 +787,7 @@ int lbc_encode(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, floa
 int lbc_forward(lbc_model* m, const float* x_dev, const float* zhat_dev, int n_img, int Hb, int Wb, float* xhat_dev,
                 float* info_dev, void* stream) {
     if (!m || !x_dev || !zhat_dev || !xhat_dev || !info_dev) return set_error(LBC_E_ARG, "null argument");
-    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
-    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");   // (no CDFs needed)
     if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;

@@ -118,7 +118,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             const int4 b = blocks[row];
             const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
             g.sym[pos] = sym;
-            g.idx[pos] = scale_index(scale, g.table);
+            g.idx[pos] = g.table ? scale_index(scale, g.table) : 0;   // no table: forward()/validation before update()
             if (g.bits) {
                 const float av = fabsf(yq - mean), sb = fmaxf(scale, 0.11f);
                 const float lik = std_cum((0.5f - av) / sb) - std_cum((-0.5f - av) / sb);

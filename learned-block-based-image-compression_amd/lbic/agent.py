@@ -87,7 +87,7 @@ class BlockBasedImgCompLossyAgent:
         self.model0 = BlockBasedImgCompLossyNetv9(config, device=self.device)
         self.lambda_ = config.lambda_
         self.rcrec_logger = RDMeter()
-        if config.mode in ("eval_model", "update_model"):
+        if config.mode in ("eval_model", "update_model", "validate_recu_reco_fast"):
             self.load_checkpoint(config.modelbest_file_load)
 
     # agents/base.py:89-128 (eval checkpoints: {'state_dict0': sd}); a missing file is loud here
@@ -107,7 +107,9 @@ class BlockBasedImgCompLossyAgent:
             return self.eval_model()
         if mode == "update_model":
             return self.update_model(force=True)
-        if mode in ("test", "validate", "validate_recu_reco", "validate_recu_reco_fast", "gen_train_set",
+        if mode == "validate_recu_reco_fast":
+            return self.validate_recu_reco_fast()
+        if mode in ("test", "validate", "validate_recu_reco", "gen_train_set",
                     "gen_train_set_postproc", "train_postproc_mdl", "train_one_acl", "train_all_acl", "debug",
                     "model_size_estimation", "flops_estimation"):
             raise NotImplementedError(f"mode {mode!r} is outside the accelerated hot path (SURVEY §2)")
@@ -174,6 +176,52 @@ class BlockBasedImgCompLossyAgent:
             self.logger.info(f"avg_psnr = {np.mean(-10 * np.log10(allrec[:, 2])):.2f}  "
                              f"avg_msssim = {np.mean(allrec[:, 4]):.8f} avg_msssimdb = {np.mean(allrec[:, 5]):.2f}")
         return allrec
+
+    @torch.no_grad()
+    def validate_recu_reco_fast(self):
+        """agents/blkbsdimgcomp_agent.py:491-528: recursive (closed-loop) reconstruction of each validation
+        image with the estimated rate of forward(), no entropy coding.  The reference's valid loader
+        center-crops to val_patch_size (dataloaders/image_dl_ACL.py:119); the crop is rounded down to whole
+        blocks here.  Loss as TrainRDLoss.forward (graphs/losses/rate_dist.py:41-50): rate + lambda * mse,
+        rate = sum(self-information) / numel(x) * 3."""
+        B = self.block_size
+        files = _list_images(self.config.valid_data)
+        mine = D.shard(list(enumerate(files)), self.rank, self.world)
+        out_dir = os.path.join(self.config.checkpoint_dir, "..", "valid_set")
+        os.makedirs(out_dir, exist_ok=True)
+        recs = []
+        for batch_idx, path in mine:
+            x = _load_image(path).to(self.device)
+            h, w = x.size(2), x.size(3)
+            ps = getattr(self.config, "val_patch_size", None)
+            if ps:
+                ch, cw = (ps, ps) if isinstance(ps, int) else (int(ps[0]), int(ps[1]))
+                ch, cw = min(ch, h), min(cw, w)
+                t, l = int(round((h - ch) / 2.0)), int(round((w - cw) / 2.0))   # torchvision CenterCrop
+                x = x[:, :, t:t + ch, l:l + cw]
+                h, w = ch, cw
+            h, w = h // B * B, w // B * B
+            x = arrange_block_pixels_to_channel_dim(x[:, :, :h, :w] - 0.5, B)
+            zhat, info = self.model0.validate_recu_reco(x)
+            mse = F.mse_loss(x, zhat).item()
+            rate = (info.sum() / x.numel() * 3).item()
+            rd_loss = rate + self.lambda_ * mse
+            psnr = 10.0 * math.log10(1.0 / mse)
+            self.logger.info("Image {:2d} --> ".format(batch_idx) +
+                             "RDLoss:{:.3f} MSE/PSNR:{:.5f}/{:.2f} Rate:{:.3f}".format(rd_loss, mse, psnr, rate))
+            img = arrange_channel_dim_to_block_pixels(zhat + 0.5, B)
+            _save_image(img[0], os.path.join(out_dir, "valid_reco_{:d}.png".format(batch_idx)))
+            recs.append([batch_idx, rd_loss, mse, rate])
+        rec = torch.tensor(recs, dtype=torch.float64, device=self.device).reshape(-1, 4)
+        allrec = D.gather_records(rec).cpu().numpy()
+        allrec = allrec[np.argsort(allrec[:, 0])]
+        if self.rank == 0:
+            for r in allrec:
+                self.rcrec_logger(r[1], r[2], r[3])
+            loss = self.rcrec_logger.display(typ="va")
+            self.logger.info(f"avg_psnr = {np.mean(-10 * np.log10(allrec[:, 2])):.2f}")
+            return loss
+        return None
 
     def finalize(self):
         self.logger.info("Please wait while finalizing the operation.. Thank you")

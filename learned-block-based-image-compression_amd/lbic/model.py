@@ -128,10 +128,14 @@ class BlockBasedImgCompLossyNetv9:
                              "(agents/blkbsdimgcomp_agent.py:481-489)")
 
     # ------------------------------------------------------------------ batched GPU path
-    def compress_batch(self, xb: torch.Tensor, want_bits: bool = False):
+    def compress_batch(self, xb: torch.Tensor, want_bits: bool = False, frame_pad: bool = False):
         """xb: [n, Hb, Wb, 3B^2] fp32 on this device.  Returns dict(streams, zhat, symbols, indexes, bits)
-        with device tensors (symbols/indexes [n, Hb*Wb*M] int32, zhat like xb)."""
-        self._check_ready()
+        with device tensors (symbols/indexes [n, Hb*Wb*M] int32, zhat like xb).  frame_pad: the closed loop of
+        validate_recu_reco (forward()'s border rule); needs no CDFs (indexes are 0 before update())."""
+        if not frame_pad:
+            self._check_ready()
+        elif self.conditional_gaussian_model._quantized_cdf.numel() and not self._tables_uploaded:
+            self._upload_tables()
         if xb.device != self.device or xb.dtype != torch.float32 or xb.dim() != 4 or xb.shape[3] != self.arch.cx:
             raise ValueError("xb must be [n, Hb, Wb, 3B^2] float32 on the model's device")
         xb = xb.contiguous()
@@ -142,9 +146,9 @@ class BlockBasedImgCompLossyNetv9:
         idx = torch.empty((n, nsym), dtype=torch.int32, device=self.device)
         bits = torch.empty((n, nsym), dtype=torch.float32, device=self.device) if want_bits else None
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().lbc_encode(self._h, _lib.ptr(xb), n, Hb, Wb, _lib.ptr(zhat), _lib.ptr(sym),
-                                         _lib.ptr(idx), _lib.ptr(bits) if bits is not None else None,
-                                         ctypes.c_void_p(stream)))
+        _lib.check(_lib.lib().lbc_encode_ex(self._h, _lib.ptr(xb), n, Hb, Wb, _lib.ptr(zhat), _lib.ptr(sym),
+                                            _lib.ptr(idx), _lib.ptr(bits) if bits is not None else None,
+                                            1 if frame_pad else 0, ctypes.c_void_p(stream)))
         return dict(zhat=zhat, symbols=sym, indexes=idx, bits=bits)
 
     def entropy_encode(self, symbols: torch.Tensor, indexes: torch.Tensor, workers: int = 0, fmt: str = "reference",
@@ -201,12 +205,25 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
+    def validate_recu_reco(self, x: torch.Tensor):
+        """The recursive reconstruction of BlockBasedImgCompLossyAgent.validate_recu_reco_fast
+        (agents/blkbsdimgcomp_agent.py:491-520): raster closed loop of forward() on causal crops, i.e. the
+        closed-loop encoder with forward()'s border semantics, no entropy coding.  x: [n, 3B^2, Hb, Wb].
+        Returns (zhat [n, 3B^2, Hb, Wb], self_information [n, M, Hb, Wb])."""
+        if x.dim() != 4 or x.shape[1] != self.arch.cx:
+            raise ValueError(f"x must be [n, {self.arch.cx}, Hb, Wb]")
+        n, _, Hb, Wb = x.shape
+        r = self.compress_batch(x.to(self.device, torch.float32).permute(0, 2, 3, 1).contiguous(), want_bits=True,
+                                frame_pad=True)
+        info = r["bits"].view(n, Hb, Wb, self.arch.M).permute(0, 3, 1, 2)
+        return r["zhat"].permute(0, 3, 1, 2), info
+
     def forward(self, zhat: torch.Tensor, x: torch.Tensor):
         """BlockBasedImgCompLossyNetv4.forward(zhat, x) (net:90-106, inherited by v9) in eval semantics:
         teacher forced on the given reconstruction, full-frame convolutions.  zhat, x: [n, 3B^2, Hb, Wb]
         (block->channel layout of arrange_block_pixels_to_channel_dim).  Returns (xhat [n, 3B^2, Hb, Wb],
-        self_information [n, M, Hb, Wb] = -log2 p), like the reference; xhat is not clamped."""
-        self._check_ready()
+        self_information [n, M, Hb, Wb] = -log2 p), like the reference; xhat is not clamped.  Needs no CDFs
+        (the reference's forward() runs before update() too)."""
         if zhat.shape != x.shape or zhat.dim() != 4 or zhat.shape[1] != self.arch.cx:
             raise ValueError(f"forward expects zhat, x of shape [n, {self.arch.cx}, Hb, Wb]")
         n, _, Hb, Wb = x.shape

@@ -233,12 +233,16 @@ class OracleNet:
         """win: [2L+1, 2L+1, C] window, c: (row, col) of the output position inside it."""
         return [win[c[0] + dy, c[1] + dx] for dy, dx in taps]
 
-    def ctx(self, win):
-        """get_meanscale_fast (net:389-398) on a (2L+1)^2 zero-padded window (valid convs)."""
+    def ctx(self, win, inside=None):
+        """get_meanscale_fast (net:389-398) on a (2L+1)^2 zero-padded window (valid convs).  inside: for
+        KS[1] = 3, a predicate on the layer-1 tap offsets (dy, dx); taps outside the frame contribute a zero
+        layer-0 vector (forward()'s 'same' zero padding, used by validate_recu_reco_fast), default: the
+        layer-0 map is evaluated on the zero-padded window (compress())."""
         L = win.shape[0] // 2
         a = self.a
         if a.KS[1] == 3:
             l0 = [_leaky(self._lin("get_meanscale.0", self._taps(win, (L + dy, L + dx), TAPS_A3)))
+                  if inside is None or inside(dy, dx) else np.zeros_like(self.conv["get_meanscale.0"][1])
                   for dy, dx in TAPS_B3]
             l1 = _leaky(self._lin("get_meanscale.2", l0))
         else:
@@ -315,11 +319,15 @@ class OracleCodec:
         L = self.a.lru
         return zp[v:v + 2 * L + 1, h:h + 2 * L + 1]
 
-    def code_block(self, zp, v, h, x):
-        """compress_blk (net:363-377) + clamp (net:357): returns sym, idx, yq, bits, xhat."""
+    def code_block(self, zp, v, h, x, frame=None):
+        """compress_blk (net:363-377) + clamp (net:357): returns sym, idx, yq, bits, xhat.  frame = (Hb, Wb):
+        forward()'s border semantics for the context net (validate_recu_reco_fast)."""
         M = self.a.M
         win = self._window(zp, v, h)
-        ksi = self.net.ctx(win)
+        inside = None
+        if frame is not None:
+            inside = lambda dy, dx: 0 <= v + dy < frame[0] and 0 <= h + dx < frame[1]
+        ksi = self.net.ctx(win, inside)
         scales, means = ksi[:M], ksi[M:]
         idx = build_indexes(scales, self.tabs.table)
         y = self.net.fwd(win, x)
@@ -328,6 +336,21 @@ class OracleCodec:
         bits = likelihood_bits(yq, scales, means)
         xhat = np.clip(self.net.inv(win, yq), F32(-0.5), F32(0.5)).astype(F32)
         return sym, idx, yq, bits, xhat
+
+    def validate_recu(self, x):
+        """validate_recu_reco_fast (agent:491-520): the raster closed loop of forward() on causal crops, which
+        is compress()'s loop with forward()'s zero padding of the context layer-0 map at the frame border.
+        x: [Hb, Wb, C].  Returns (zhat [Hb, Wb, C], self-information [Hb, Wb, M])."""
+        Hb, Wb, C = x.shape
+        L = self.a.lru
+        zp = np.zeros((Hb + 2 * L, Wb + 2 * L, C), F32)
+        info = np.zeros((Hb, Wb, self.a.M), F32)
+        for v in range(Hb):
+            for h in range(Wb):
+                _, _, _, bits, xhat = self.code_block(zp, v, h, x[v, h], frame=(Hb, Wb))
+                zp[v + L, h + L] = xhat
+                info[v, h] = bits
+        return zp[L:L + Hb, L:L + Wb].copy(), info
 
     def compress(self, x, rows=None, with_bytes=True):
         """x: [Hb, Wb, C] fp32.  Returns dict(bytes, zhat, symbols [Hb*Wb*M], indexes, bits).

@@ -16,6 +16,8 @@ Fixtures written:
   stages_b8_lowrate.npz  per-stage activations of compress_blk for a few blocks of the 2-row B8 frame
   forward_<name>.npz     the reference's teacher-forced forward(zhat, x) (net:90-106, eval mode) on a given
                          zhat: xhat and self-information -log2 p, full-frame conv semantics
+  recu_<name>.npz        the recursive reconstruction of validate_recu_reco_fast (agent:491-528): the closed
+                         loop of forward() on the causal crops, zhat and self-information per block
 """
 from __future__ import annotations
 
@@ -245,10 +247,62 @@ def gen_forward(name, arch, H, W, seed0):
         x=bm(x), zhat=bm(zhat), xhat=bm(xhat), self_info=bm(self_info))
 
 
+RECUS = {
+    "tiny_ks3111": (Arch(4, (3, 1, 1, 1), 64, 16), 24, 28, 900),
+    "tiny_ks3311": (Arch(4, (3, 3, 1, 1), 64, 16), 24, 28, 1000),
+}
+
+
+def gen_recu(name, arch, H, W, seed0):
+    """validate_recu_reco_fast's loop (agent:491-520) around the reference model: for every block in raster
+    order, model0(zhat crop, x crop) on the causal crop [v-U..v] x [h-L..h+R] (LRU from get_lru_(KS,
+    'validation'), agent:480-488), the block's output clamped into zhat and its self-information kept.
+    Tie screening: the teacher-forced forward(zhat_final, x) evaluates every block exactly as the loop did
+    (masked convs never read the not-yet-reconstructed blocks), so its margins are the loop's."""
+    sd = synth_state_dict(arch, WEIGHT_SEED)
+    model, net = refshim.make_model(arch, sd)
+    model.update(force=True)
+    LRU = sum(k // 2 for k in arch.KS) + sum(k // 2 for k in arch.KS[1:])
+    seed = seed0
+    while True:
+        img = synth_image(seed, H, W)
+        x = to_blocks(img, arch.B)
+        _, _, hg, wd = x.shape
+        zhat = torch.zeros_like(x)
+        info = torch.zeros(1, arch.M, hg, wd)
+        with torch.no_grad():
+            for v in range(hg):
+                for h in range(wd):
+                    LL, RR, UU = max(0, h - LRU), min(wd, h + LRU + 1), max(0, v - LRU)
+                    xh, si = model(zhat[:, :, UU:v + 1, LL:RR], x[:, :, UU:v + 1, LL:RR])
+                    info[:, :, v, h] = si[:, :, v - UU, h - LL]
+                    zhat[:, :, v, h] = xh[:, :, v - UU, h - LL].clamp_(-0.5, 0.5)
+            rec = Recorder(model.conditional_gaussian_model)
+            model(zhat, x)
+        d = np.concatenate(rec.d)
+        margin = np.abs(np.abs(d - np.floor(d)) - 0.5).min()
+        model.conditional_gaussian_model.quantize = rec._q
+        model.conditional_gaussian_model.build_indexes = rec._b
+        print(f"recu {name}: seed {seed} margin {margin:.2e}", flush=True)
+        if margin > TIE_EPS:
+            break
+        seed += 1
+        assert seed < seed0 + 400, "no tie-free seed found"
+    bm = lambda t: t[0].permute(1, 2, 0).contiguous().numpy()
+    np.savez_compressed(
+        os.path.join(HERE, f"recu_{name}.npz"),
+        B=arch.B, KS=np.array(arch.KS), N=arch.N, M=arch.M, weight_seed=WEIGHT_SEED, image_seed=seed,
+        x=bm(x), zhat=bm(zhat), self_info=bm(info))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     gen_cdf(os.path.join(HERE, "cdf_pmf.npz"))
     only = sys.argv[1:]
+    for name, (arch, H, W, s0) in RECUS.items():
+        if only and ("recu_" + name) not in only:
+            continue
+        gen_recu(name, arch, H, W, s0)
     for name, (arch, H, W, s0) in FORWARDS.items():
         if only and ("forward_" + name) not in only:
             continue

@@ -37,3 +37,26 @@ def test_main_eval_model(tmp_path, monkeypatch, caplog):
     assert any("SYNTHETIC" in l for l in lines)              # missing checkpoint is loud
     assert (tmp_path / "experiments" / "tiny" / "exp_100.0" / "checkpoints" / "missing.pth.tar_updated").exists()
     assert (tmp_path / "experiments" / "tiny" / "exp_100.0" / "test" / "img0.png").exists()
+
+
+def test_main_validate_recu_reco_fast(tmp_path, monkeypatch, caplog):
+    """mode validate_recu_reco_fast through main.py: one log line per image and the 'Valid Epoch' summary."""
+    from PIL import Image
+    import main as lbic_main
+    data = tmp_path / "val"
+    data.mkdir()
+    rng = np.random.default_rng(4)
+    for k in range(2):
+        Image.fromarray(rng.integers(0, 256, (40, 36, 3), dtype=np.uint8)).save(data / f"v{k}.png")
+    cfg = dict(exp_name="recu", agent="BlockBasedImgCompLossyAgent", net_version="v9", mode="validate_recu_reco_fast",
+               cuda=True, gpu_device=0, seed=1337, block_size=4, KS=[3, 3, 1, 1], N=64, M=16, use_postpm=False,
+               lambda_=100.0, val_patch_size=32, modelbest_file_load="missing.pth.tar", valid_data=str(data))
+    p = tmp_path / "cfg.json"
+    p.write_text(json.dumps(cfg))
+    monkeypatch.chdir(tmp_path)
+    with caplog.at_level(logging.INFO):
+        lbic_main.main([str(p)])
+    lines = [r.getMessage() for r in caplog.records]
+    assert sum(l.startswith("Image ") and "RDLoss:" in l for l in lines) == 2
+    assert any("Valid Epoch" in l for l in lines)
+    assert any(l.startswith("avg_psnr") for l in lines)

@@ -284,3 +284,24 @@ def test_bad_inputs_raise():
         m.forward(x.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2)[:, :, :1])
     # the handle still works afterwards
     assert torch.equal(m.decompress_batch(st, Hb, Wb), r["zhat"])
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+def test_validate_recu_reco_matches_reference(name):
+    """The recursive reconstruction of validate_recu_reco_fast on the GPU against the reference's own loop:
+    zhat within 1e-5, self-information within 1e-4 relative; teacher-forced forward() on its result
+    reproduces it bit for bit (same semantics by construction); for KS3111 it equals compress()."""
+    g = load_golden("recu_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    x = torch.from_numpy(g["x"]).permute(2, 0, 1)[None].cuda()
+    zhat, info = m.validate_recu_reco(x)
+    z = zhat[0].permute(1, 2, 0).cpu().numpy()
+    inf = info[0].permute(1, 2, 0).cpu().numpy()
+    assert np.abs(z - g["zhat"]).max() < 1e-5
+    assert (np.abs(inf - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
+    xhat, info_f = m.forward(zhat, x)
+    assert torch.equal(torch.clamp(xhat, -0.5, 0.5), zhat) and torch.equal(info_f, info)
+    if arch.KS[1] == 1:
+        r = m.compress_batch(x.permute(0, 2, 3, 1).contiguous(), want_bits=True)
+        assert torch.equal(r["zhat"].permute(0, 3, 1, 2), zhat)

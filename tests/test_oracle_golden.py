@@ -124,3 +124,15 @@ def test_oracle_forward_matches_reference(name):
     xhat, info = net.forward_frame(g["zhat"], g["x"])
     assert np.abs(xhat - g["xhat"]).max() < 1e-5
     assert (np.abs(info - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+def test_oracle_validate_recu_matches_reference(name):
+    """validate_recu_reco_fast (agent:491-520) semantics: the oracle's closed loop with forward()'s border
+    rule against the reference's loop around its own forward()."""
+    g = load_golden("recu_" + name)
+    arch = golden_arch(g)
+    codec = O.OracleCodec(arch, synth_state_dict(arch, int(g["weight_seed"])))
+    z, info = codec.validate_recu(g["x"])
+    assert np.abs(z - g["zhat"]).max() < 1e-5
+    assert (np.abs(info - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
