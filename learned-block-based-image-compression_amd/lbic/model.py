@@ -196,8 +196,9 @@ class BlockBasedImgCompLossyNetv9:
             raise ValueError(f"unknown bitstream format {fmt!r}")
         self._check_ready()
         n = len(streams)
-        bufs = [ctypes.create_string_buffer(bytes(s), len(s)) for s in streams]
-        arr = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        # pointers into the callers' bytes objects (no copies); `bufs` keeps them alive during the call
+        bufs = [s if isinstance(s, bytes) else bytes(s) for s in streams]
+        arr = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
         lens = (ctypes.c_size_t * n)(*[len(s) for s in streams])
         zhat = torch.empty((n, Hb, Wb, self.arch.cx), dtype=torch.float32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
