@@ -60,6 +60,26 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+struct HostPinned {          // page-locked staging buffer (bitstreams -> device by DMA)
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~HostPinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    int alloc(size_t b) {
+        if (b <= bytes && p) return LBC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipHostMalloc(&p, std::max<size_t>(b, 16), hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return set_error(LBC_E_HIP, "hipHostMalloc failed");
+        }
+        bytes = b;
+        return LBC_OK;
+    }
+};
+
 struct Layer {
     DevBuf W, bias;
     int K = 0, N = 0, NB16 = 0;
@@ -126,6 +146,7 @@ struct lbc_model {
     // per-shape workspace
     int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
     DevBuf zpad, blocks_enc, blocks_dec;
+    HostPinned stage;           // bitstream staging (upload_streams)
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -393,11 +414,14 @@ int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, siz
         std::memcpy(w, subs[i].first, 8);
         x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
     }
-    std::vector<uint8_t> cat(total);
-    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat.data() + off, subs[i].first, subs[i].second);
     int rc;
-    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
-    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
+    // the previous call's copy out of the staging buffer must be done before it is overwritten
+    HIPCHK(hipStreamSynchronize(s));
+    if ((rc = m->stage.alloc(total + total / 2 + (1 << 20)))) return rc;
+    uint8_t* cat = static_cast<uint8_t*>(m->stage.p);
+    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat + off, subs[i].first, subs[i].second);
+    if (total > m->words.bytes && (rc = m->words.alloc(total + total / 2 + (1 << 20)))) return rc;
+    HIPCHK(hipMemcpyAsync(m->words.p, cat, total, hipMemcpyHostToDevice, s));
     // per-stream arrays: sized by the stream count, pointers kept stable for the graphs
     const size_t cap = std::max<size_t>(n, 64);
     if ((rc = m->word_base.alloc(cap * sizeof(long long))) || (rc = m->word_count.alloc(cap * sizeof(int))) ||
