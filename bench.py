@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
+    ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
+                    help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
     ap.add_argument("--substream-steps", type=int, default=2,
                     help="extra steps in the opt-in per-row sub-stream format, reported apart (0 = skip)")
@@ -129,6 +131,8 @@ def main():
     # two codec handles (own workspaces and reconstruction buffers): the encoder side and the decoder side
     # of the two-stage pipeline; the decoder gets its own HIP stream
     enc_model, dec_model = make_model(), make_model()
+    if not args.serial and args.enc_lds_floor:
+        enc_model.set_encoder_lds_floor(args.enc_lds_floor)
     s_enc, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
     n = args.batch

@@ -76,6 +76,12 @@ int lbc_set_entropy_tables(lbc_model *m, const float *scale_table, int n_tables,
 int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, float *zhat_dev,
                int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, void *stream);
 
+/* Options.  LBC_OPT_ENC_LDS_FLOOR (bytes, 0..160 KB): LDS reserved by each workgroup of the encoder's
+ * large-M GEMM; above 80 KB one encoder workgroup per CU, which leaves room for a decoder running
+ * concurrently on another stream (bench.py's two-stage pipeline).  Results are unchanged. */
+#define LBC_OPT_ENC_LDS_FLOOR 1
+int lbc_set_option(lbc_model *m, int option, long long value);
+
 /* lbc_encode with flags.  LBC_ENC_FRAME_PAD: the context net's layer-0 map is zero outside the frame
  * (forward()'s 'same' padding) instead of being evaluated on the zero-padded zhat (compress()): the closed
  * loop of validate_recu_reco_fast (agents/blkbsdimgcomp_agent.py:491-520), which runs forward() on causal

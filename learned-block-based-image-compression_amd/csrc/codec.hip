@@ -60,26 +60,6 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-struct HostPinned {          // page-locked staging buffer (bitstreams -> device by DMA)
-    void* p = nullptr;
-    size_t bytes = 0;
-    ~HostPinned() {
-        if (p) (void)hipHostFree(p);
-    }
-    int alloc(size_t b) {
-        if (b <= bytes && p) return LBC_OK;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-        if (hipHostMalloc(&p, std::max<size_t>(b, 16), hipHostMallocDefault) != hipSuccess) {
-            p = nullptr;
-            return set_error(LBC_E_HIP, "hipHostMalloc failed");
-        }
-        bytes = b;
-        return LBC_OK;
-    }
-};
-
 struct Layer {
     DevBuf W, bias;
     int K = 0, N = 0, NB16 = 0;
@@ -142,11 +122,12 @@ struct lbc_model {
     int total16 = 0;
     std::vector<uint16_t> c16_host;
     std::vector<int> meta_host;
+    int lut16 = 0;              // start-index LUT entries after the CDF rows (long tables only)
     bool tabs_dirty = false;
     // per-shape workspace
     int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
     DevBuf zpad, blocks_enc, blocks_dec;
-    HostPinned stage;           // bitstream staging (upload_streams)
+    int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -381,6 +362,7 @@ RansArgs rans_args(lbc_model* m) {
     RansArgs r{};
     r.cdf16 = m->cdf16_dev.as<uint16_t>();
     r.tmeta = m->tmeta_dev.as<int>();
+    r.lut16 = m->lut16;
     r.total16 = m->total16;
     r.words = m->words.as<uint32_t>();
     r.word_base = m->word_base.as<long long>();
@@ -414,14 +396,13 @@ int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, siz
         std::memcpy(w, subs[i].first, 8);
         x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
     }
+    std::vector<uint8_t> cat(total);
+    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat.data() + off, subs[i].first, subs[i].second);
     int rc;
-    // the previous call's copy out of the staging buffer must be done before it is overwritten
-    HIPCHK(hipStreamSynchronize(s));
-    if ((rc = m->stage.alloc(total + total / 2 + (1 << 20)))) return rc;
-    uint8_t* cat = static_cast<uint8_t*>(m->stage.p);
-    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat + off, subs[i].first, subs[i].second);
-    if (total > m->words.bytes && (rc = m->words.alloc(total + total / 2 + (1 << 20)))) return rc;
-    HIPCHK(hipMemcpyAsync(m->words.p, cat, total, hipMemcpyHostToDevice, s));
+    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
+    // (a page-locked staging buffer here corrupted the stamp slots of the other codec handle's encoder
+    // graph on ROCm 7.2 — a reproducible, unexplained interaction; the pageable copy is kept)
+    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
     // per-stream arrays: sized by the stream count, pointers kept stable for the graphs
     const size_t cap = std::max<size_t>(n, 64);
     if ((rc = m->word_base.alloc(cap * sizeof(long long))) || (rc = m->word_count.alloc(cap * sizeof(int))) ||
@@ -461,6 +442,7 @@ GemmArgs base_args(lbc_model* m, const int4* blocks, int rows, const float* x, i
     g.table = m->table_dev.as<float>();
     g.Mlat = m->M;
     g.HW = Hb * Wb;
+    g.lds_floor = m->enc_lds_floor;
     (void)n_img;
     return g;
 }
@@ -624,6 +606,17 @@ int lbc_create(const lbc_config* cfg, lbc_model** out) {
     return LBC_OK;
 }
 
+int lbc_set_option(lbc_model* m, int option, long long value) {
+    if (!m) return set_error(LBC_E_ARG, "null argument");
+    switch (option) {
+        case LBC_OPT_ENC_LDS_FLOOR:
+            if (value < 0 || value > 160 * 1024) return set_error(LBC_E_ARG, "LDS floor out of range [0, 160 KB]");
+            m->enc_lds_floor = (int)value;
+            return LBC_OK;
+    }
+    return set_error(LBC_E_ARG, "unknown option");
+}
+
 void lbc_destroy(lbc_model* m) {
     if (!m) return;
     for (auto& e : m->ev)
@@ -710,7 +703,7 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
     t.offset.assign(offset, offset + n_tables);
     // device copies: scale table, and 16-bit CDF rows for the GPU rANS decoder
     std::vector<uint16_t> c16;
-    std::vector<int> meta(3 * 64, 0);
+    std::vector<int> meta(4 * 64, 0);
     for (int i = 0; i < n_tables; ++i) {
         const int len = t.length[i];
         if (len < 3 || len > cdf_stride) return set_error(LBC_E_ARG, "bad cdf length");
@@ -727,8 +720,12 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
     while (c16.size() & 7) c16.push_back(0);   // 16-byte granules for the LDS staging loads
     {   // the decoder's start-index LUT follows the tables (k_rans_decode stages both into LDS)
         std::vector<uint16_t> lut;
-        build_start_lut(t, lut);
+        std::vector<int> lut_off;
+        build_start_lut(t, lut, lut_off);
+        while (lut.size() & 7) lut.push_back(0);
+        for (int i = 0; i < n_tables; ++i) meta[192 + i] = lut_off[i];
         m->total16 = (int)c16.size();
+        m->lut16 = (int)lut.size();
         c16.insert(c16.end(), lut.begin(), lut.end());
     }
     if (c16.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
@@ -765,7 +762,8 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     // the graph works on library-owned buffers only, so it survives new caller tensors
     const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->x_in.p, (long long)m->zpad.p,
                                         (long long)m->sym_buf.p, (long long)m->lane[0].ctx0.p,
-                                        (long long)m->table_dev.p, m->prof.sample_every, flags};
+                                        (long long)m->table_dev.p, m->prof.sample_every, flags,
+                                        m->enc_lds_floor};
     if (!m->enc_exec || key != m->enc_key) {
         if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
         HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
@@ -895,6 +893,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             r.cdf16 = m->cdf16_dev.as<uint16_t>();
             r.tmeta = m->tmeta_dev.as<int>();
             r.total16 = m->total16;
+            r.lut16 = m->lut16;
             r.words = m->words.as<uint32_t>();
             r.word_base = m->word_base.as<long long>();
             r.word_count = m->word_count.as<int>();

@@ -63,15 +63,17 @@ struct GemmArgs {
     float* bits;
     int HW;
     Geo geo;
+    int lds_floor;           // k_gemm: LDS bytes to reserve per workgroup (caps residency, lbc_set_option)
     int zero_oob;            // EPI_LEAKY: rows whose context position lies outside the frame are written as 0
                              // (forward()'s zero padding of the layer-0 map, KS[1] = 3)
 };
 
 struct RansArgs {
     const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit),
-                             // then the 64 x 256 start-index LUT (build_start_lut)
-    const int* tmeta;        // [3][64]: base, cdf_length, offset
-    int total16;             // entries in cdf16 (even)
+                             // then the start-index LUT rows of the long tables (build_start_lut)
+    const int* tmeta;        // [4][64]: base, cdf_length, offset, LUT row offset (-1: short table, no LUT)
+    int total16;             // CDF entries in cdf16 (multiple of 8)
+    int lut16;               // LUT entries after them (multiple of 8)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;
     const int* word_count;

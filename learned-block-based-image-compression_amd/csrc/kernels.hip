@@ -463,11 +463,12 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
 
 template <int BM, int BN, int NW, int CH>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
-    const size_t lds = (size_t)KSPLIT * BM * BN * sizeof(float);
+    const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
+    if (lds > 160 * 1024) return set_error(LBC_E_ARG, "LDS request above 160 KB");
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
@@ -568,6 +569,7 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     const int Mlat = a.Mlat;
     // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
     const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
+    const int t_lut = a.tmeta[192 + lane];
     const unsigned long long x_in = a.state_x[img];
     const int p_in = a.state_ptr[img];
     const long long wb = a.word_base[img];
@@ -582,7 +584,7 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     {   // CDF tables + start-index LUT (both built on the host, contiguous in cdf16)
         const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = threadIdx.x; i < (a.total16 + 64 * 256) / 8; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (a.total16 + a.lut16) / 8; i += blockDim.x) dst[i] = src[i];
     }
     unsigned long long x = uni64(x_in);
     int p = __builtin_amdgcn_readfirstlane(p_in);
@@ -626,9 +628,12 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
             const int len = __builtin_amdgcn_readlane(t_len, ci);
             const int off = __builtin_amdgcn_readlane(t_off, ci);
             const uint32_t cum = (uint32_t)(x & 0xffff);
-            // window start: the symbol at the start of cum's 256-wide bucket (host-built LUT)
-            int lo = llut[ci * 256 + (cum >> 8)];
+            // window start: the symbol at the start of cum's 256-wide bucket (host-built LUT; a short
+            // table has none and its whole CDF fits the window from 0)
+            const int lut = __builtin_amdgcn_readlane(t_lut, ci);
+            int lo = llut[max(lut, 0) + (cum >> 8)];
             lo = __builtin_amdgcn_readfirstlane(lo);
+            lo = lut < 0 ? 0 : lo;
             RSTAMP(t1)
             RACC(0, t1 - t0);
             uint32_t c;
@@ -695,8 +700,8 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     if (a.rows <= 0) return LBC_OK;     // an empty wavefront step (e.g. odd steps of a one-column frame)
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
-    if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 table must be padded to 16 bytes");
-    const size_t lds = (size_t)(a.total16 + 64 * 256) * sizeof(uint16_t);
+    if (a.total16 % 8 || a.lut16 % 8) return set_error(LBC_E_ARG, "cdf16 tables must be padded to 16 bytes");
+    const size_t lds = (size_t)(a.total16 + a.lut16) * sizeof(uint16_t);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),

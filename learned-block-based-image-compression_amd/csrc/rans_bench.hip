@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 64; ++i)
         for (size_t j = 0; j < cdfs[i].size(); ++j) t.cdf[(size_t)i * maxlen + j] = (int32_t)cdfs[i][j];
     std::vector<uint16_t> c16;
-    std::vector<int> meta(192);
+    std::vector<int> meta(256);
     for (int i = 0; i < 64; ++i) {
         meta[i] = (int)c16.size(); meta[64 + i] = t.length[i]; meta[128 + i] = t.offset[i];
         for (int j = 0; j < t.length[i] - 1; ++j) c16.push_back((uint16_t)t.cdf[(size_t)i * maxlen + j]);
@@ -54,7 +54,12 @@ int main(int argc, char** argv) {
     }
     while (c16.size() & 7) c16.push_back(0);
     const int total16 = (int)c16.size();
-    { std::vector<uint16_t> lut; build_start_lut(t, lut); c16.insert(c16.end(), lut.begin(), lut.end()); }
+    std::vector<uint16_t> lut;
+    std::vector<int> lut_off;
+    build_start_lut(t, lut, lut_off);
+    while (lut.size() & 7) lut.push_back(0);
+    for (int i = 0; i < 64; ++i) meta[192 + i] = lut_off[i];
+    c16.insert(c16.end(), lut.begin(), lut.end());
     // symbols: index uniform over the table, value ~ N(0, 1.2 sigma)
     std::mt19937 rng(1);
     std::vector<int32_t> idx((size_t)n_img * steps * M), sym(idx.size());
@@ -88,6 +93,7 @@ int main(int argc, char** argv) {
     a.cdf16 = (const uint16_t*)up(c16.data(), c16.size() * 2);
     a.tmeta = (const int*)up(meta.data(), meta.size() * 4);
     a.total16 = total16;
+    a.lut16 = (int)lut.size();
     a.words = (const uint32_t*)up(words.data(), words.size() * 4);
     a.word_base = (const long long*)up(base.data(), base.size() * 8);
     a.word_count = (const int*)up(cnt.data(), cnt.size() * 4);

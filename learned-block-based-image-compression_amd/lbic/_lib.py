@@ -43,6 +43,7 @@ _SIGS = {
                     ctypes.c_int, _P, _P], ctypes.c_int),
     "lbc_encode_ex": ([_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int, _P],
                       ctypes.c_int),
+    "lbc_set_option": ([_P, ctypes.c_int, ctypes.c_longlong], ctypes.c_int),
     "lbc_forward": ([_P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P], ctypes.c_int),
     "lbc_rans_encode_rows": ([_P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P),
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),

@@ -206,6 +206,11 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
+    def set_encoder_lds_floor(self, nbytes: int):
+        """LBC_OPT_ENC_LDS_FLOOR: LDS reserved per encoder GEMM workgroup (> 80 KB: one per CU, leaving
+        room for a decoder on another stream).  Performance only; results are unchanged."""
+        _lib.check(_lib.lib().lbc_set_option(self._h, 1, int(nbytes)))
+
     def validate_recu_reco(self, x: torch.Tensor):
         """The recursive reconstruction of BlockBasedImgCompLossyAgent.validate_recu_reco_fast
         (agents/blkbsdimgcomp_agent.py:491-520): raster closed loop of forward() on causal crops, i.e. the
