@@ -5,10 +5,12 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU.  One step = the reference's timed region of eval_model
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
-GPU rANS decode).  Steps are software-pipelined two deep (default): while batch k is decoded (latency-bound
-raster chain, few CUs busy) batch k+1 is compressed and entropy coded on another stream/handle; the timed
-region holds exactly `steps` compressions and `steps` decompressions (--serial: no overlap; a serial
-measurement is also reported under "serial_schedule").  Inputs are resident in HBM when the timed region starts.  Weights are the seeded
+GPU rANS decode).  Batches are software-pipelined (default --depth 2): two batch decodes are in flight
+(latency-bound raster chains, each on its own codec handle and HIP stream, few CUs busy) while the next
+batches are compressed and entropy coded on a third handle/stream; the timed region holds exactly `steps`
+compressions and `steps` decompressions.  The one-decode-in-flight pipeline and the non-overlapped serial
+schedule are reported beside it ("two_stage_schedule", "serial_schedule"; --depth 1 / --serial select them).
+Inputs are resident in HBM when the timed region starts.  Weights are the seeded
 synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
 checkpoints offline).
 
@@ -82,7 +84,7 @@ def cpu_baseline(arch, sd, H, W, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
@@ -91,6 +93,9 @@ def main():
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; 3+ serialises on "
+                         "ROCm 7.2's 4 hardware queues per process)")
     ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
                     help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
@@ -128,12 +133,18 @@ def main():
         m.update(force=True)
         return m
 
-    # two codec handles (own workspaces and reconstruction buffers): the encoder side and the decoder side
-    # of the two-stage pipeline; the decoder gets its own HIP stream
-    enc_model, dec_model = make_model(), make_model()
-    if not args.serial and args.enc_lds_floor:
+    # codec handles with their own workspaces and reconstruction buffers: one encoder side and `depth`
+    # decoder sides of the pipeline, each on its own HIP stream (created back to back so they land on
+    # distinct hardware queues)
+    depth = 0 if args.serial else args.depth
+    enc_model = make_model()
+    dec_models = [make_model() for _ in range(max(depth, 1))]
+    if depth and args.enc_lds_floor:
         enc_model.set_encoder_lds_floor(args.enc_lds_floor)
-    s_enc, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s_enc = torch.cuda.Stream(dev)
+    s_decs = [torch.cuda.Stream(dev) for _ in dec_models]
+    handles = [enc_model] + dec_models
+    plock = threading.Lock()
 
     n = args.batch
     frames = np.stack([image_to_blocks(np.random.default_rng(rank * n + k).integers(0, 256, (3, H, W), dtype=np.uint8)
@@ -161,86 +172,124 @@ def main():
             s_enc.synchronize()
             t1 = time.perf_counter()
             st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
-        ph["encode"] += t1 - t0
-        ph["entropy"] += time.perf_counter() - t1
+        t2 = time.perf_counter()
+        with plock:
+            ph["encode"] += t1 - t0
+            ph["entropy"] += t2 - t1
         return r, st
 
-    def decode_side(st, fmt, ph, out):
+    def decode_side(i, st, fmt, ph):
         t0 = time.perf_counter()
-        with torch.cuda.stream(s_dec):
-            z = dec_model.decompress_batch(st, Hb, Wb, fmt=fmt)
-            s_dec.synchronize()
-        ph["decode"] += time.perf_counter() - t0
-        out.append(z)
+        with torch.cuda.stream(s_decs[i]):
+            z = dec_models[i].decompress_batch(st, Hb, Wb, fmt=fmt)
+            s_decs[i].synchronize()
+        with plock:
+            ph["decode"] += time.perf_counter() - t0
+        return z
 
     def collect_stats():
         ks = {}
-        for m_ in (enc_model, dec_model):           # merge the two handles' per-kernel records
+        for m_ in handles:           # merge the handles' per-kernel records
             for name, st_ in (m_.profile_end() or {}).items():
                 acc = ks.setdefault(name, dict(launches=0, total_launches=0, total_ms=0.0, flops=0.0, bytes=0.0))
                 for k_ in acc:
                     acc[k_] += st_[k_]
         return ks
 
-    def run(fmt, steps, warmup, pipelined, label, prof=False):
-        """`steps` timed batches.  Pipelined: step k decodes batch k-1 (decoder stream, helper thread; ctypes
-        drops the GIL) while batch k is compressed and entropy coded (encoder stream, this thread), so the
-        timed region holds exactly `steps` encodes and `steps` decodes; the pipeline is primed with one
-        encode and drained with one decode outside it.  Serial: encode, entropy, decode one after another."""
+    def run(fmt, steps, warmup, depth, label, prof=False):
+        """`steps` timed batches.  depth 0: encode, entropy, decode one after another.  depth D >= 1: a software
+        pipeline -- D decoder handles (own streams, helper threads; ctypes drops the GIL) decode batches in
+        order from a queue of at most D encoded batches, while this thread compresses and entropy codes the
+        next ones.  The timed region holds exactly `steps` encodes and `steps` decodes: the pipeline is primed
+        with D encodes and drained with D decodes outside it (its steady state)."""
         ph = dict(encode=0.0, entropy=0.0, decode=0.0)
         scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
         for i in range(warmup):
-            r, st = encode_side(fmt, scratch)
-            decode_side(st, fmt, scratch, [])
+            for d in range(len(dec_models)):          # every decoder handle builds its graphs
+                r, st = encode_side(fmt, scratch)
+                decode_side(d, st, fmt, scratch)
             log(f"[rank {rank}] {label} warmup {i + 1}/{warmup} done")
-        prev = encode_side(fmt, scratch) if pipelined else None     # prime: batch 0 encoded
-        last = None
         if prof:      # launch counts cover the timed region only (same sampling period: graphs are kept)
-            for m_ in (enc_model, dec_model):
+            for m_ in handles:
                 m_.profile_begin(args.sample_every)
+        last = []
+        if depth == 0:
+            barrier()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                r, st = encode_side(fmt, ph)
+                last = [(r, st, decode_side(0, st, fmt, ph))]
+                log(f"[rank {rank}] {label} step {i + 1}/{steps}: {time.perf_counter() - t0:.2f} s")
+            barrier()
+            dt = max_over_ranks(time.perf_counter() - t0)
+            return dt, ph, (last[-1] if last else None), collect_stats() if prof else None
+        import queue
+        pending = [encode_side(fmt, scratch) for _ in range(depth)]      # prime
+        q = queue.Queue(maxsize=depth)
+        done = []
+
+        def decoder(i):
+            while True:
+                item = q.get()
+                if item is None:
+                    return
+                j, (r_, st_) = item
+                z_ = decode_side(i, st_, fmt, ph)
+                with plock:
+                    done.append((j, r_, st_, z_))
+                log(f"[rank {rank}] {label} batch {j} decoded (decoder {i}): {time.perf_counter() - t0:.2f} s")
+
+        fed = [0]
+
+        def feed():
+            while pending and fed[0] < steps:
+                q.put((fed[0], pending.pop(0)))
+                fed[0] += 1
+
+        ths = [threading.Thread(target=decoder, args=(i,)) for i in range(depth)]
         barrier()
         t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        feed()
         for i in range(steps):
-            if pipelined:
-                out = []
-                th = threading.Thread(target=decode_side, args=(prev[1], fmt, ph, out))
-                th.start()
-                cur = encode_side(fmt, ph)
-                th.join()
-                last = (prev[0], prev[1], out[0])
-                prev = cur
-            else:
-                r, st = encode_side(fmt, ph)
-                out = []
-                decode_side(st, fmt, ph, out)
-                last = (r, st, out[0])
-            log(f"[rank {rank}] {label} step {i + 1}/{steps}: {time.perf_counter() - t0:.2f} s")
+            pending.append(encode_side(fmt, ph))
+            feed()
+        for _ in ths:
+            q.put(None)
+        for th in ths:
+            th.join()
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         ks = collect_stats() if prof else None
-        if pipelined:                                               # drain (outside the timed region)
-            decode_side(prev[1], fmt, scratch, [])
-        return dt, ph, last, ks
+        for k, (r_, st_) in enumerate(pending):                        # drain (outside the timed region)
+            decode_side(k % depth, st_, fmt, scratch)
+        j, r_, st_, z_ = max(done, key=lambda e: e[0])
+        return dt, ph, (r_, st_, z_), ks
 
     # sampling is part of the captured graphs: enable it before the warmup builds them
-    for m_ in (enc_model, dec_model):
+    for m_ in handles:
         m_.profile_begin(args.sample_every)
-    pipelined = not args.serial
-    run("reference", 0, args.warmup, False, "warmup")
-    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, pipelined, "reference", prof=True)
-    serial = None
-    if pipelined and args.serial_steps > 0:     # the same batches without the overlap, for reference
-        dts, phs, _, _ = run("reference", args.serial_steps, 0, False, "serial")
-        serial = dict(value=round(world * n * H * W / (dts / args.serial_steps) / 1e6, 4),
-                      ms_per_step=round(dts / args.serial_steps * 1e3, 2), steps=args.serial_steps,
-                      phases_ms_per_step={k: round(v / args.serial_steps * 1e3, 2) for k, v in phs.items()})
+    run("reference", 0, args.warmup, 0, "warmup")
+    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, depth, "reference", prof=True)
+
+    def summary(dts, phs, k):
+        return dict(value=round(world * n * H * W / (dts / k) / 1e6, 4), ms_per_step=round(dts / k * 1e3, 2),
+                    steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in phs.items()})
+    serial = two_stage = None
+    if depth and args.serial_steps > 0:     # the same batches without the overlap, for reference
+        dts, phs, _, _ = run("reference", args.serial_steps, 0, 0, "serial")
+        serial = summary(dts, phs, args.serial_steps)
+    if depth > 1 and args.serial_steps > 0:  # one decoder in flight
+        dts, phs, _, _ = run("reference", 2 * args.serial_steps, 0, 1, "two-stage")
+        two_stage = summary(dts, phs, 2 * args.serial_steps)
 
     # --- opt-in sub-stream format (SURVEY H1b): same encoder, one rANS stream per block row, wavefront
     #     decode.  Reported apart from the headline (which stays on the reference bitstream format).
     sub = None
     if args.substream_steps > 0:
-        run("rows", 0, 1, False, "rows warmup")
-        dts, phs, (rs, ss, zs), _ = run("rows", args.substream_steps, 0, pipelined, "rows")
+        run("rows", 0, 1, 0, "rows warmup")
+        dts, phs, (rs, ss, zs), _ = run("rows", args.substream_steps, 0, depth, "rows")
         sub = dict(value=round(world * n * H * W / (dts / args.substream_steps) / 1e6, 4),
                    ms_per_step=round(dts / args.substream_steps * 1e3, 2), steps=args.substream_steps,
                    bpp=round(float(np.mean([len(b) * 8.0 / (H * W) for b in ss])), 5),
@@ -325,9 +374,11 @@ def main():
                                "encode+decode in the reference bitstream format (one raster rANS stream per image)",
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
                    "global_batch": n * world,
-                   "schedule": "serial: encode, entropy, decode per batch" if args.serial else
-                   "two-stage pipeline: batch k+1 compress + host rANS overlaps batch k decode (2 codec handles, "
-                   "2 HIP streams); each timed step = one full encode and one full decode of a 32-frame batch"},
+                   "schedule": "serial: encode, entropy, decode per batch" if depth == 0 else
+                   f"software pipeline: {depth} batch decode(s) in flight (one codec handle + HIP stream each) "
+                   "beside the compress + host rANS of the next batches (own handle + stream); each timed step = "
+                   f"one full encode and one full decode of a {n}-frame batch",
+                   "decode_batches_in_flight": depth},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"bpp": round(bpp, 5), "psnr_db": round(psnr, 3), "enc_dec_bit_exact": bit_exact},
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
@@ -335,6 +386,7 @@ def main():
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
         "kernels": kernels,
         "serial_schedule": serial,
+        "two_stage_schedule": two_stage,
         "substream_format": sub,
     }
     print(json.dumps(out), flush=True)

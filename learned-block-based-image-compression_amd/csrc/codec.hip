@@ -335,7 +335,7 @@ int prof_range_begin(Prof* p, int r, hipStream_t s) {
     p->next = 0;
     for (auto& c : p->per_replay[r]) c = 0;
     if (p->sample_every && p->slots)
-        HIPCHK(hipMemsetAsync(p->slots + kSlotU64 * (size_t)r * kSlotsPerRange, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange, s));
+        return launch_zero_u64(p->slots + kSlotU64 * (size_t)r * kSlotsPerRange, kSlotU64 * kSlotsPerRange, s);
     return LBC_OK;
 }
 
@@ -1081,6 +1081,9 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
         HIPCHK(hipSetDevice(m->cfg.device));
         HIPCHK(hipMalloc(&p.slots, 8 * kSlotU64 * (size_t)kSlotsPerRange * kRanges));
         HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * kRanges));
+        if (getenv("LBIC_DEBUG_STAMPS"))
+            fprintf(stderr, "handle %p slots %p..%p\n", (void*)m, (void*)p.slots,
+                    (void*)(p.slots + kSlotU64 * (size_t)kSlotsPerRange * kRanges));
     }
     // sample_every is part of the graph keys: a change re-captures (and re-creates the sample records);
     // an unchanged value only restarts the launch counting
@@ -1111,7 +1114,7 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
                 if (d >= 0 && d > span) span = d;
             }
             if (getenv("LBIC_DEBUG_STAMPS") && span > 10000000) {
-                fprintf(stderr, "bad slot %d cls %d:", r.slot, r.cls);
+                fprintf(stderr, "handle %p bad slot %d cls %d:", (void*)m, r.slot, r.cls);
                 for (int x = 0; x < 16; ++x) fprintf(stderr, " %llx", t[x]);
                 fprintf(stderr, "\n");
             }

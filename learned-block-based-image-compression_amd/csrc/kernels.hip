@@ -715,6 +715,19 @@ int launch_rans_decode(const RansArgs& a, hipStream_t s) {
 
 __global__ void k_ctr_add(int* c, int d) { *c += d; }
 
+// zeroes n 64-bit words (the timing-slot range at the head of a sampled graph: a captured memset node
+// there wrote a stale 16-byte fill pattern into the range when several threads replayed graphs)
+__global__ void k_zero_u64(unsigned long long* p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0ull;
+}
+
+int launch_zero_u64(unsigned long long* p, int n, hipStream_t s) {
+    if (n <= 0) return LBC_OK;
+    hipLaunchKernelGGL(k_zero_u64, dim3((n + 255) / 256), dim3(256), 0, s, p, n);
+    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "zero launch failed");
+}
+
 int launch_ctr_add(int* ctr, int d, hipStream_t s) {
     hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, s, ctr, d);
     return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "ctr launch failed");
