@@ -122,7 +122,6 @@ struct lbc_model {
     int total16 = 0;
     std::vector<uint16_t> c16_host;
     std::vector<int> meta_host;
-    int lut16 = 0;              // start-index LUT entries after the CDF rows (long tables only)
     bool tabs_dirty = false;
     // per-shape workspace
     int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
@@ -362,7 +361,6 @@ RansArgs rans_args(lbc_model* m) {
     RansArgs r{};
     r.cdf16 = m->cdf16_dev.as<uint16_t>();
     r.tmeta = m->tmeta_dev.as<int>();
-    r.lut16 = m->lut16;
     r.total16 = m->total16;
     r.words = m->words.as<uint32_t>();
     r.word_base = m->word_base.as<long long>();
@@ -701,34 +699,11 @@ int lbc_set_entropy_tables(lbc_model* m, const float* scale_table, int n_tables,
     t.cdf.assign(cdf, cdf + (size_t)n_tables * cdf_stride);
     t.length.assign(cdf_length, cdf_length + n_tables);
     t.offset.assign(offset, offset + n_tables);
-    // device copies: scale table, and 16-bit CDF rows for the GPU rANS decoder
+    // device copies: scale table, and the GPU rANS decoder's LDS image of the CDF rows
     std::vector<uint16_t> c16;
-    std::vector<int> meta(4 * 64, 0);
-    for (int i = 0; i < n_tables; ++i) {
-        const int len = t.length[i];
-        if (len < 3 || len > cdf_stride) return set_error(LBC_E_ARG, "bad cdf length");
-        meta[i] = (int)c16.size();
-        meta[64 + i] = len;
-        meta[128 + i] = t.offset[i];
-        for (int j = 0; j < len - 1; ++j) {
-            const int32_t v = cdf[(size_t)i * cdf_stride + j];
-            if (v < 0 || v > 65535) return set_error(LBC_E_ARG, "cdf entry out of 16-bit range");
-            c16.push_back((uint16_t)v);
-        }
-        c16.push_back(0);   // slot of the implicit final 2^16
-    }
-    while (c16.size() & 7) c16.push_back(0);   // 16-byte granules for the LDS staging loads
-    {   // the decoder's start-index LUT follows the tables (k_rans_decode stages both into LDS)
-        std::vector<uint16_t> lut;
-        std::vector<int> lut_off;
-        build_start_lut(t, lut, lut_off);
-        while (lut.size() & 7) lut.push_back(0);
-        for (int i = 0; i < n_tables; ++i) meta[192 + i] = lut_off[i];
-        m->total16 = (int)c16.size();
-        m->lut16 = (int)lut.size();
-        c16.insert(c16.end(), lut.begin(), lut.end());
-    }
-    if (c16.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
+    std::vector<int> meta;
+    if (int rc = build_rans_gpu_tables(t, c16, meta)) return rc;
+    m->total16 = (int)c16.size();
     m->c16_host = std::move(c16);
     m->meta_host = std::move(meta);
     m->tabs_set = true;
@@ -893,8 +868,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             r.cdf16 = m->cdf16_dev.as<uint16_t>();
             r.tmeta = m->tmeta_dev.as<int>();
             r.total16 = m->total16;
-            r.lut16 = m->lut16;
-            r.words = m->words.as<uint32_t>();
+                    r.words = m->words.as<uint32_t>();
             r.word_base = m->word_base.as<long long>();
             r.word_count = m->word_count.as<int>();
             r.state_x = m->st_x.as<unsigned long long>();

@@ -149,26 +149,44 @@ int rans_decode_host(const EntropyTables& t, const uint8_t* data, size_t len, co
     return LBC_OK;
 }
 
-// For the GPU decoder: per table, the symbol index whose interval contains cum = 256*q (q = 0..255),
-// i.e. the largest s with cdf[s] <= 256*q.  A symbol with cum in bucket q lies in [lut[q], lut[q+1]].
-// Start-index LUT of the GPU decoder: for each table whose CDF has more than 64 entries, 256 buckets of
-// cum (cum >> 8) -> the last symbol s with cdf[s] <= 256*bucket (the 64-entry window search starts there).
-// Short tables need none (their whole CDF fits one window): lut_off[i] = -1.  Keeping only the long
-// tables' rows halves the decoder's LDS footprint (87 -> 71 KB for the 64 Gaussian tables).
-void build_start_lut(const EntropyTables& t, std::vector<uint16_t>& lut, std::vector<int>& lut_off) {
-    lut.clear();
-    lut_off.assign(t.n_tables, -1);
-    for (int i = 0; i < t.n_tables; ++i) {
-        if (t.length[i] - 1 <= 64) continue;
-        lut_off[i] = (int)lut.size();
+// LDS image of the GPU decoder's tables (k_rans_decode, kernels.hip).  Every CDF entry c is stored as the
+// 16-bit e = c - 1 (mod 2^16): c <= cum  <=>  e < cum for every c >= 1, the only c = 0 entry (index 0)
+// becomes 0xFFFF and is never counted (the decoder counts lane 0 of a window itself), and the implicit
+// final 2^16 is also 0xFFFF (and e + 1 = 2^16 recovers it).
+//   coarse [n_tables][64]  lane l of table t: e[min(l * S_t, len_t - 1)], 0xFFFF past the table
+//   fine   per table: e[0 .. len_t - 2], then 64 x 0xFFFF (so a 64-wide window never leaves the table)
+// S_t = ceil((len_t - 1) / 64) symbols per coarse segment; a table with len_t <= 64 is "short": its coarse
+// row is its whole CDF (S = 1).
+// meta [5][64]: fine row start (bytes), S (in bytes: 2 S), len - 2 (the escape symbol), coarse row start (bytes),
+// offset (-pmf_center).
+int build_rans_gpu_tables(const EntropyTables& t, std::vector<uint16_t>& img, std::vector<int>& meta) {
+    const int nt = t.n_tables;
+    if (nt < 1 || nt > 64) return set_error(LBC_E_ARG, "GPU rANS decoder supports 1..64 tables");
+    img.assign((size_t)nt * 64, 0xFFFF);
+    meta.assign(5 * 64, 0);
+    for (int i = 0; i < nt; ++i) {
+        const int len = t.length[i];
+        if (len < 3 || len > t.stride) return set_error(LBC_E_ARG, "bad cdf length");
+        if (len - 1 > 63 * 64) return set_error(LBC_E_ARG, "cdf longer than the GPU decoder's 2-level search");
         const int32_t* cdf = t.cdf.data() + (size_t)i * t.stride;
-        int s = 0;
-        for (int q = 0; q < 256; ++q) {
-            const int32_t c = 256 * q;
-            while (s + 1 <= t.length[i] - 2 && cdf[s + 1] <= c) ++s;
-            lut.push_back((uint16_t)s);
-        }
+        if (cdf[0] != 0 || cdf[len - 1] != 65536) return set_error(LBC_E_ARG, "cdf must span [0, 2^16]");
+        for (int j = 0; j + 1 < len; ++j)
+            if (cdf[j + 1] <= cdf[j]) return set_error(LBC_E_ARG, "cdf must be strictly increasing");
+        const size_t fbase = img.size();
+        for (int j = 0; j < len - 1; ++j) img.push_back((uint16_t)((cdf[j] - 1) & 0xFFFF));
+        for (int j = 0; j < 64; ++j) img.push_back(0xFFFF);
+        const bool shrt = len <= 64;
+        const int S = shrt ? 1 : (len - 1 + 63) / 64;
+        for (int l = 0; l < 64; ++l) img[(size_t)i * 64 + l] = img[fbase + std::min(l * S, len - 1)];
+        meta[i] = (int)fbase * 2;
+        meta[64 + i] = S * 2;
+        meta[128 + i] = len - 2;
+        meta[192 + i] = i * 128;
+        meta[256 + i] = t.offset[i];
     }
+    while (img.size() & 7) img.push_back(0xFFFF);   // 16-byte granules for the LDS staging loads
+    if (img.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");
+    return LBC_OK;
 }
 
 }  // namespace lbic

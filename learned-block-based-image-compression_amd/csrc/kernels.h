@@ -69,11 +69,11 @@ struct GemmArgs {
 };
 
 struct RansArgs {
-    const uint16_t* cdf16;   // all tables, concatenated (entries < 2^16; the final 2^16 is implicit),
-                             // then the start-index LUT rows of the long tables (build_start_lut)
-    const int* tmeta;        // [4][64]: base, cdf_length, offset, LUT row offset (-1: short table, no LUT)
-    int total16;             // CDF entries in cdf16 (multiple of 8)
-    int lut16;               // LUT entries after them (multiple of 8)
+    const uint16_t* cdf16;   // LDS image of the tables (build_rans_gpu_tables: coarse rows, then padded
+                             // fine rows, entries stored as cdf - 1)
+    const int* tmeta;        // [5][64] per table: fine row start, 2 S (S = symbols per coarse lane), cdf_length - 2,
+                             // coarse row start (starts in bytes of the image), offset (-pmf_center)
+    int total16;             // entries in cdf16 (multiple of 8)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;
     const int* word_count;

@@ -519,42 +519,53 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
 }
 
 // ----------------------------------------------------------------------------------------- rANS decode
-// One 64-lane wave per image decodes that image's Mlat symbols of the current block (RansDecoder::
-// decode_stream, called per block at net:439), entirely on the GPU.  Up to 8 images share a workgroup
-// and one LDS copy of the 16-bit CDF tables.  Per symbol: one wave-wide window compare (ballot +
-// popcount) around the table centre gives the symbol, v_readlane pulls its CDF interval out of the
-// window, and the next 64 stream words sit lane-distributed in a register (renormalisation is a
-// readlane, not a dependent global load).  The 64-bit state is wave-uniform.  Output:
-// y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
+// One 64-lane wave per stream (reference format: one per image) decodes the Mlat symbols of the current
+// block (RansDecoder::decode_stream, called per block at net:439), entirely on the GPU.  Up to 8 streams
+// share a workgroup and one LDS copy of the tables (build_rans_gpu_tables: CDF entries stored as c - 1,
+// a 64-entry coarse row per table, fine rows padded with 0xFFFF).  The 64-bit state is wave-uniform
+// (SGPRs); one wave issues about one instruction per 4 cycles, so the per-symbol body is kept short and
+// everything that does not depend on the state is done a symbol ahead:
+//   * before the loop, every lane gathers the table metadata of "its" symbols (lane i of chunk kb =
+//     symbol 64 kb + i); per symbol the next symbol's metadata is a v_readlane and its coarse row an
+//     LDS read issued while the current symbol waits for its own fine read;
+//   * level 1: cum against the prefetched coarse row (one compare + popcount) picks a segment of S
+//     symbols; level 2: one 64-wide LDS window read from that segment start, compare + popcount gives
+//     the symbol, two v_readlanes its interval (a short table, <= 64 entries, has S = 1);
+//   * the block's stream words are staged in LDS with the tables; renormalisation takes the next word
+//     from there, requested as soon as the previous one is consumed.
+// Output: y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
 #ifndef LBIC_RANS_WPB
 #define LBIC_RANS_WPB 8
 #endif
-constexpr int RANS_WPB = LBIC_RANS_WPB;   // waves (images) per workgroup
-constexpr int RANS_MAXLAT = 256; // Mlat <= 4 * 64
+constexpr int RANS_WPB = LBIC_RANS_WPB;   // waves (streams) per workgroup
+constexpr int RANS_MAXLAT = 256;          // Mlat <= 4 * 64
+constexpr int RANS_WIN = 512;             // stream words staged in LDS per wave and launch (>= 52/32 * MAXLAT)
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ int rdlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {   // keep a uniform value in SGPRs
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
     return ((unsigned long long)hi << 32) | lo;
 }
 
-#ifdef LBIC_RANS_STAMPS
-__device__ unsigned long long* g_rdbg;
-#define RSTAMP(var)                                                                                   \
-    unsigned long long var;                                                                         \
-    __builtin_amdgcn_sched_barrier(0);                                                              \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");                      \
-    __builtin_amdgcn_sched_barrier(0);
-#define RACC(k, d) acc[k] += (d)
-#else
-#define RSTAMP(var)
-#define RACC(k, d)
-#endif
 // Called by every wave of the workgroup (rows past a.rows only help fill the LDS tables): the wave's
-// stream state is requested first, the workgroup then copies the CDF tables + LUT into LDS while those
-// loads are in flight, and only the stream window (which depends on them) waits for the barrier.
+// stream state and indexes are requested first, the workgroup then copies the tables into LDS while those
+// loads are in flight.
+#ifdef LBIC_RANS_STAMPS
+__device__ unsigned long long* g_rdbg;   // diagnostic build (rans_bench): per wave s_memtime at 4 points
+#define RSTAMP(k)                                                                                    \
+    do {                                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                  \
+        if (lane == 0 && row_in < a.rows) g_rdbg[row_in * 4 + (k)] = t_;                             \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+    } while (0)
+#else
+#define RSTAMP(k) do {} while (0)
+#endif
 __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int row_in, int lane) {
+    RSTAMP(0);
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
     // stream / state of this row: the image's (reference format: row = image) or the block row's
@@ -567,125 +578,151 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     }
     img = __builtin_amdgcn_readfirstlane(img);
     const int Mlat = a.Mlat;
-    // per-table metadata, lane t holds table t (read with v_readlane, no dependent scalar loads)
-    const int t_base = a.tmeta[lane], t_len = a.tmeta[64 + lane], t_off = a.tmeta[128 + lane];
-    const int t_lut = a.tmeta[192 + lane];
+    // per-table metadata, lane t holds table t
+    const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
+    const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane];
     const unsigned long long x_in = a.state_x[img];
     const int p_in = a.state_ptr[img];
     const long long wb = a.word_base[img];
     const int nw_in = a.word_count[img];
-    int idxr[4], symr[4];
+    // table of symbol i (ti) and of symbol i + 1 (tn: the next symbol's metadata is read a symbol ahead)
+    int ti[4], tn[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
-        idxr[kb] = i < Mlat ? a.idx[(long)row * Mlat + i] : 0;
-        symr[kb] = 0;
-    }
-    {   // CDF tables + start-index LUT (both built on the host, contiguous in cdf16)
-        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
-        uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = threadIdx.x; i < (a.total16 + a.lut16) / 8; i += blockDim.x) dst[i] = src[i];
+        // clamped, unconditional loads (indexes are 0..63 by construction; entries past Mlat are unused)
+        ti[kb] = a.idx[(long)row * Mlat + min(i, Mlat - 1)] & 63;
+        tn[kb] = a.idx[(long)row * Mlat + min(i + 1, Mlat - 1)] & 63;
     }
     unsigned long long x = uni64(x_in);
     int p = __builtin_amdgcn_readfirstlane(p_in);
     const uint32_t* w = a.words + wb;
     const int nw = __builtin_amdgcn_readfirstlane(nw_in);
-    int p0 = p;
-    uint32_t wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
-    __syncthreads();
-    if (!valid) return;
-    const uint16_t* lcdf = lds;
-    const uint16_t* llut = lds + a.total16;
-    int bad = 0;
-#ifdef LBIC_RANS_STAMPS
-    unsigned long long acc[4] = {0, 0, 0, 0};
-#endif
-    // next stream word (lane-distributed window of 64 words; reloaded every 64 words)
-    auto next_word = [&]() -> uint32_t {
-        if (p - p0 >= 64) {
-            p0 = p;
-            wbuf = (p0 + lane < nw) ? w[p0 + lane] : 0u;
+    const int p0 = p;
+    {   // tables (one LDS image built on the host) and this wave's stream words p0 .. p0 + RANS_WIN - 1
+        // (0 past the stream's end; a block never needs more: <= 52 bits per symbol incl. a bypass
+        // escape), so renormalisation reads LDS at a uniform address instead of global memory.  Loads
+        // are clamped and unconditional and all issued before the first LDS store (a guarded load, or a
+        // load -> store pair per iteration, would wait for each load in turn).
+        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        const int n16 = a.total16 / 8, bd = blockDim.x;
+        uint32_t* win = reinterpret_cast<uint32_t*>(lds + a.total16) + (threadIdx.x >> 6) * RANS_WIN;
+        uint32_t wv[RANS_WIN / 64];
+#pragma unroll
+        for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
+        for (int i0 = threadIdx.x; i0 < n16; i0 += 8 * bd) {
+            uint4 r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = src[min(i0 + k * bd, n16 - 1)];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[min(i0 + k * bd, n16 - 1)] = r[k];   // past the end: a duplicate
         }
-        const uint32_t v = p < nw ? rdlane(wbuf, p - p0) : 0u;
-        bad |= p >= nw;
-        ++p;
-        return v;
-    };
-    auto get_bits = [&](int nb) -> uint32_t {
-        const uint32_t v = (uint32_t)(x & ((1u << nb) - 1));
-        x >>= nb;
-        if (x < (1ull << 31)) x = (x << 32) | next_word();
-        x = uni64(x);
-        return v;
-    };
+#pragma unroll
+        for (int k = 0; k < RANS_WIN / 64; ++k) win[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
+    }
+    // symbol-major metadata (gathered from the table lanes): lane i of chunk kb = symbol 64 kb + i + 1
+    // (fine row start, S, escape symbol, coarse row start); the offset of symbol 64 kb + i itself
+    int nfbv[4], nSv[4], nlmv[4], ncav[4], moff[4], symv[4];
+    int fb, S, lm2, ca0;
+    {
+        const int sel0 = __builtin_amdgcn_readfirstlane(ti[0]);
+        fb = rdlane_i(t_fb, sel0); S = rdlane_i(t_S, sel0); lm2 = rdlane_i(t_lm2, sel0); ca0 = rdlane_i(t_ca, sel0);
+    }
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-        const int cnt_i = min(64, Mlat - kb * 64);
-        for (int ii = 0; ii < cnt_i; ++ii) {
-            RSTAMP(t0)
-            const int ci = __builtin_amdgcn_readlane(idxr[kb], ii) & 63;     // indexes are 0..63 by construction
-            const int base = __builtin_amdgcn_readlane(t_base, ci);
-            const int len = __builtin_amdgcn_readlane(t_len, ci);
-            const int off = __builtin_amdgcn_readlane(t_off, ci);
-            const uint32_t cum = (uint32_t)(x & 0xffff);
-            // window start: the symbol at the start of cum's 256-wide bucket (host-built LUT; a short
-            // table has none and its whole CDF fits the window from 0)
-            const int lut = __builtin_amdgcn_readlane(t_lut, ci);
-            int lo = llut[max(lut, 0) + (cum >> 8)];
-            lo = __builtin_amdgcn_readfirstlane(lo);
-            lo = lut < 0 ? 0 : lo;
-            RSTAMP(t1)
-            RACC(0, t1 - t0);
-            uint32_t c;
-            int cnt;
-            for (;;) {
-                const int j = lo + lane;
-                // unconditional LDS read (the LUT behind the last table keeps base + j in bounds),
-                // entries past the table's end act as 2^16
-                const uint32_t raw = lcdf[base + j];
-                c = j < len - 1 ? raw : 65536u;
-                cnt = __popcll(__ballot(c <= cum));
-                if (cnt < 64) break;
-                lo += 63;
+        const int sel = tn[kb] << 2;
+        nfbv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
+        nSv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
+        nlmv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
+        ncav[kb] = __builtin_amdgcn_ds_bpermute(sel, t_ca);
+        moff[kb] = __builtin_amdgcn_ds_bpermute(ti[kb] << 2, t_off);
+        symv[kb] = 0;
+    }
+    __syncthreads();
+    if (!valid) return;
+    RSTAMP(1);
+    int bad = 0;
+    const uint32_t* win = reinterpret_cast<const uint32_t*>(lds + a.total16) + (threadIdx.x >> 6) * RANS_WIN;
+    // words q0 .. q0 + 63 of the LDS window lane-distributed in a register; wn = the word renormalisation
+    // takes next (a v_readlane, prepared as soon as the previous word is consumed)
+    int q0 = 0;
+    uint32_t wbuf = win[lane];
+    uint32_t wn = rdlane(wbuf, 0);
+    auto renorm = [&]() {
+        uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);   // 0 <=> x < RANS64_L = 2^31
+        asm("" : "+s"(t));               // keep the test on the scalar unit (not a 64-bit VALU compare)
+        if (t == 0) {
+            x = (x << 32) | wn;
+            ++p;
+            if (p - p0 - q0 >= 64) {     // next 64 words (rare: a stall of one LDS read)
+                q0 = min(q0 + 64, RANS_WIN - 64);
+                wbuf = win[q0 + lane];
             }
-            RSTAMP(t2)
-            RACC(1, t2 - t1);
-            const int sidx = lo + cnt - 1;
-            const uint32_t start = rdlane(c, cnt - 1), nxt = rdlane(c, cnt);
-            x = (unsigned long long)(nxt - start) * (x >> 16) + (x & 0xffff) - start;
-            if (x < (1ull << 31)) x = (x << 32) | next_word();
-            x = uni64(x);
-            RSTAMP(t3)
-            RACC(2, t3 - t2);
-            int v = sidx;
-            if (v == len - 2) {   // escape: value coded in 4-bit bypass chunks
-                uint32_t cc = get_bits(4), nb = cc;
-                while (cc == 15u && nb <= 8) { cc = get_bits(4); nb += cc; }
+            wn = rdlane(wbuf, min(p - p0 - q0, 63));
+        }
+        x = uni64(x);
+    };
+    const char* lb = reinterpret_cast<const char*>(lds);
+    const int lane2 = lane * 2;
+    uint32_t cv = *reinterpret_cast<const uint16_t*>(lb + ca0 + lane2);   // coarse row of symbol 0
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int cnt_i = __builtin_amdgcn_readfirstlane(min(64, Mlat - kb * 64));
+        if (cnt_i <= 0) break;
+        for (int ii = 0; ii < cnt_i; ++ii) {
+            const uint32_t cum = (uint32_t)x & 0xffffu;
+            // level 1: segment j (coarse lane 0 is never counted: j = #entries <= cum, minus one)
+            const int j = __popcll(__ballot(cv < cum));
+            const int sbb = j * S;                  // segment start (bytes; fb and S are in bytes)
+            const uint32_t fine = *reinterpret_cast<const uint16_t*>(lb + fb + sbb + lane2);
+            // next symbol's metadata and coarse row, in the shadow of the fine read
+            const int nfb = rdlane_i(nfbv[kb], ii), nS = rdlane_i(nSv[kb], ii);
+            const int nlm2 = rdlane_i(nlmv[kb], ii), nca = rdlane_i(ncav[kb], ii);
+            const uint32_t cvn = *reinterpret_cast<const uint16_t*>(lb + nca + lane2);
+            __builtin_amdgcn_sched_barrier(0);   // both LDS reads issued before the fine read is waited for
+            // level 2: the window from the segment start (lane 0 is <= cum by construction; a short
+            // table has S = 1, so its window always answers kk = 0)
+            const int kk = __popcll(__ballot(fine < cum) | 1ull) - 1;
+            const int s = (sbb >> 1) + kk;
+            const uint32_t start = (rdlane(fine, kk) + 1u) & 0xffffu;   // e + 1 = c (the c = 0 entry wraps)
+            const uint32_t nxt = rdlane(fine, kk + 1) + 1u;
+            x = (unsigned long long)(nxt - start) * (x >> 16) + (cum - start);
+            renorm();
+            int v = s;
+            if (__builtin_expect(s == lm2, 0)) {   // escape: value coded in 4-bit bypass chunks
+                auto get_bits = [&]() -> uint32_t {
+                    const uint32_t b = (uint32_t)(x & 15u);
+                    x >>= 4;
+                    renorm();
+                    return b;
+                };
+                uint32_t cc = get_bits(), nb = cc;
+                while (cc == 15u && nb <= 8) { cc = get_bits(); nb += cc; }
                 if (nb > 8) { bad |= 4; nb = 0; }
                 uint32_t raw = 0;
-                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits(4) << (jj * 4);
+                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits() << (jj * 4);
                 v = (int)(raw >> 1);
-                v = (raw & 1) ? -v - 1 : v + len - 2;
+                v = (raw & 1) ? -v - 1 : v + lm2;
             }
-            if (lane == ii) symr[kb] = v + off;
-            RSTAMP(t4)
-            RACC(3, t4 - t3);
+            symv[kb] = lane == ii ? v : symv[kb];
+            fb = nfb; S = nS; lm2 = nlm2; cv = cvn;
         }
     }
+    RSTAMP(2);
+    bad |= p > nw;                       // consumed words past the end of the stream
+    bad |= (p - p0 > RANS_WIN) ? 8 : 0;  // (cannot happen: <= 52 bits per symbol)
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
-        if (i < Mlat) a.yq[(long)row * a.ldy + i] = (float)symr[kb] + a.ksi[(long)row * a.ldk + Mlat + i];
+        if (i < Mlat) a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
     }
-#ifdef LBIC_RANS_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < 4; ++k) g_rdbg[row * 4 + k] = acc[k];
-#endif
     if (lane == 0) {
         a.state_x[img] = x;
         a.state_ptr[img] = p;
         if (bad) a.status[img] = bad;
     }
+    RSTAMP(3);
 }
 
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
@@ -700,8 +737,8 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     if (a.rows <= 0) return LBC_OK;     // an empty wavefront step (e.g. odd steps of a one-column frame)
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
-    if (a.total16 % 8 || a.lut16 % 8) return set_error(LBC_E_ARG, "cdf16 tables must be padded to 16 bytes");
-    const size_t lds = (size_t)(a.total16 + a.lut16) * sizeof(uint16_t);
+    if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 tables must be padded to 16 bytes");
+    const size_t lds = (size_t)a.total16 * sizeof(uint16_t) + (size_t)RANS_WPB * RANS_WIN * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),

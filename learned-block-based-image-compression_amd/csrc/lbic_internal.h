@@ -28,6 +28,6 @@ int rans_encode(const EntropyTables& t, const int32_t* symbols, const int32_t* i
 int rans_decode_host(const EntropyTables& t, const uint8_t* data, size_t len, const int32_t* indexes, size_t n,
                      int32_t* out);
 
-void build_start_lut(const EntropyTables& t, std::vector<uint16_t>& lut, std::vector<int>& lut_off);
+int build_rans_gpu_tables(const EntropyTables& t, std::vector<uint16_t>& img, std::vector<int>& meta);
 
 }  // namespace lbic
