@@ -535,11 +535,12 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
 //     from there, requested as soon as the previous one is consumed.
 // Output: y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
 #ifndef LBIC_RANS_WPB
-#define LBIC_RANS_WPB 8
+#define LBIC_RANS_WPB 4   // one wave per SIMD: a lone wave issues its latency-bound chain ~13 % faster than two
 #endif
 constexpr int RANS_WPB = LBIC_RANS_WPB;   // waves (streams) per workgroup
 constexpr int RANS_MAXLAT = 256;          // Mlat <= 4 * 64
 constexpr int RANS_WIN = 512;             // stream words staged in LDS per wave and launch (>= 52/32 * MAXLAT)
+constexpr int RANS_FILL = 8192 / (RANS_WPB * 64);   // 16-byte table loads per thread in flight (128 KB per pass)
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ int rdlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -594,29 +595,35 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
         ti[kb] = a.idx[(long)row * Mlat + min(i, Mlat - 1)] & 63;
         tn[kb] = a.idx[(long)row * Mlat + min(i + 1, Mlat - 1)] & 63;
     }
+    // LDS staging: the tables (one image built on the host) and this wave's stream words p0 .. p0 +
+    // RANS_WIN - 1 (0 past the stream's end; a block never needs more: <= 52 bits per symbol incl. a
+    // bypass escape), so renormalisation reads LDS at a uniform address instead of global memory.  The
+    // first table chunk is requested before anything waits (it depends on nothing), the words as soon as
+    // the stream position has arrived; loads are clamped and unconditional and all issued before the
+    // first LDS store (a guarded load, or a load -> store pair per iteration, waits for each in turn).
+    const uint4* tsrc = reinterpret_cast<const uint4*>(a.cdf16);
+    uint4* tdst = reinterpret_cast<uint4*>(lds);
+    const int n16 = a.total16 / 8, bd = blockDim.x;
+    uint4 r[RANS_FILL];
+#pragma unroll
+    for (int k = 0; k < RANS_FILL; ++k) r[k] = tsrc[min((int)threadIdx.x + k * bd, n16 - 1)];
     unsigned long long x = uni64(x_in);
     int p = __builtin_amdgcn_readfirstlane(p_in);
     const uint32_t* w = a.words + wb;
     const int nw = __builtin_amdgcn_readfirstlane(nw_in);
     const int p0 = p;
-    {   // tables (one LDS image built on the host) and this wave's stream words p0 .. p0 + RANS_WIN - 1
-        // (0 past the stream's end; a block never needs more: <= 52 bits per symbol incl. a bypass
-        // escape), so renormalisation reads LDS at a uniform address instead of global memory.  Loads
-        // are clamped and unconditional and all issued before the first LDS store (a guarded load, or a
-        // load -> store pair per iteration, would wait for each load in turn).
-        const uint4* src = reinterpret_cast<const uint4*>(a.cdf16);
-        uint4* dst = reinterpret_cast<uint4*>(lds);
-        const int n16 = a.total16 / 8, bd = blockDim.x;
+    {
         uint32_t* win = reinterpret_cast<uint32_t*>(lds + a.total16) + (threadIdx.x >> 6) * RANS_WIN;
         uint32_t wv[RANS_WIN / 64];
 #pragma unroll
         for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
-        for (int i0 = threadIdx.x; i0 < n16; i0 += 8 * bd) {
-            uint4 r[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) r[k] = src[min(i0 + k * bd, n16 - 1)];
+        for (int k = 0; k < RANS_FILL; ++k) tdst[min((int)threadIdx.x + k * bd, n16 - 1)] = r[k];   // past the end: a duplicate
+        for (int i0 = threadIdx.x + RANS_FILL * bd; i0 < n16; i0 += RANS_FILL * bd) {   // tables > RANS_FILL chunks
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dst[min(i0 + k * bd, n16 - 1)] = r[k];   // past the end: a duplicate
+            for (int k = 0; k < RANS_FILL; ++k) r[k] = tsrc[min(i0 + k * bd, n16 - 1)];
+#pragma unroll
+            for (int k = 0; k < RANS_FILL; ++k) tdst[min(i0 + k * bd, n16 - 1)] = r[k];
         }
 #pragma unroll
         for (int k = 0; k < RANS_WIN / 64; ++k) win[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
