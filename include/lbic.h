@@ -109,6 +109,14 @@ int lbc_rans_encode(const lbc_model *m, const int32_t *sym, const int32_t *idx, 
 int lbc_rans_decode_host(const lbc_model *m, const uint8_t *data, size_t len, const int32_t *idx, size_t n,
                          int32_t *sym_out);
 
+/* RansDecoder.decode_with_indexes (CompressAI C++; called once per block at net:439) on the GPU, for
+ * n_streams independent streams at once: chunk c decodes the next M symbols (M = the model's latent
+ * channels) of every stream with the table indexes idx_dev[c][stream][M] and writes the symbols to
+ * sym_dev[c][stream][M] (both device int32).  The same k_rans_decode kernel lbc_decode runs per raster
+ * step; streams are host bitstreams as lbc_rans_encode produced.  Returns LBC_E_STREAM for an overrun. */
+int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_streams,
+                        const int32_t *idx_dev, int n_chunks, int32_t *sym_dev, void *stream);
+
 /* decompress() (net:400-452) for a batch of images: streams[i] / lens[i] are the host bitstreams
  * lbc_rans_encode produced.  Strictly raster-serial within an image (the reference format has one
  * rANS stream per image); images are decoded together, rANS decode runs on the GPU. */

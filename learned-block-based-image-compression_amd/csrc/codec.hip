@@ -828,6 +828,28 @@ int lbc_rans_decode_host(const lbc_model* m, const uint8_t* data, size_t len, co
     return rans_decode_host(m->tabs, data, len, idx, n, sym_out);
 }
 
+int lbc_rans_decode_gpu(lbc_model* m, const uint8_t* const* streams, const size_t* lens, int n_streams,
+                        const int32_t* idx_dev, int n_chunks, int32_t* sym_dev, void* stream) {
+    if (!m || !streams || !lens || !idx_dev || !sym_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_streams <= 0 || n_chunks < 0) return set_error(LBC_E_ARG, "bad stream / chunk count");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    std::vector<std::pair<const uint8_t*, size_t>> subs;
+    for (int i = 0; i < n_streams; ++i) subs.emplace_back(streams[i], lens[i]);
+    if ((rc = upload_streams(m, subs, s))) return rc;
+    RansArgs r = rans_args(m);
+    r.rows = n_streams;
+    for (int c = 0; c < n_chunks && !rc; ++c) {
+        r.idx = idx_dev + (size_t)c * n_streams * m->M;
+        r.sym_out = sym_dev + (size_t)c * n_streams * m->M;
+        rc = launch_rans_decode(r, s);
+    }
+    if (rc) return rc;
+    return check_status(m, (size_t)n_streams, s);
+}
+
 int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, int n_img, int Hb, int Wb,
                float* zhat_dev, void* stream) {
     if (!m || !streams || !lens || !zhat_dev) return set_error(LBC_E_ARG, "null argument");

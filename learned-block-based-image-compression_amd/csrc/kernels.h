@@ -85,6 +85,7 @@ struct RansArgs {
     int ldk, Mlat;
     float* yq;
     int ldy;
+    int32_t* sym_out;        // non-null: write the decoded symbols [rows][Mlat] instead of y_qnt
     const int4* blocks;
     const int* ctr;
     int ctr_stride;

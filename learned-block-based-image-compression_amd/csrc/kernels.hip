@@ -722,7 +722,10 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
-        if (i < Mlat) a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
+        if (i < Mlat) {
+            if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
+            else a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
+        }
     }
     if (lane == 0) {
         a.state_x[img] = x;

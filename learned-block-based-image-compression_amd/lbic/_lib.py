@@ -39,6 +39,8 @@ _SIGS = {
     "lbc_rans_encode": ([_P, _P, _P, ctypes.c_size_t, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t)],
                         ctypes.c_int),
     "lbc_rans_decode_host": ([_P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P], ctypes.c_int),
+    "lbc_rans_decode_gpu": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, _P,
+                             ctypes.c_int, _P, _P], ctypes.c_int),
     "lbc_decode": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                     ctypes.c_int, _P, _P], ctypes.c_int),
     "lbc_encode_ex": ([_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int, _P],

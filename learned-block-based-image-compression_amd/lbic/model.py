@@ -206,6 +206,24 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
+    def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
+        """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]
+        int32 (chunk c = the next M symbols of every stream, as one raster step of decompress) ->
+        symbols [C, n, M] int32 on the model's device (lbc_rans_decode_gpu; the decoder's own kernel)."""
+        self._check_ready()
+        n = len(streams)
+        idx = indexes.to(self.device, torch.int32).contiguous()
+        if idx.dim() != 3 or idx.shape[1] != n or idx.shape[2] != self.arch.M:
+            raise ValueError(f"indexes must be [chunks, {n}, {self.arch.M}]")
+        bufs = [s if isinstance(s, bytes) else bytes(s) for s in streams]
+        arr = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+        lens = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+        sym = torch.empty_like(idx)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(_lib.lib().lbc_rans_decode_gpu(self._h, arr, lens, n, _lib.ptr(idx), idx.shape[0], _lib.ptr(sym),
+                                                   ctypes.c_void_p(stream)))
+        return sym
+
     def set_encoder_lds_floor(self, nbytes: int):
         """LBC_OPT_ENC_LDS_FLOOR: LDS reserved per encoder GEMM workgroup (> 80 KB: one per CU, leaving
         room for a decoder on another stream).  Performance only; results are unchanged."""
