@@ -914,6 +914,9 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
                 GemmArgs g = base_args(m, blocks, rows, nullptr, n_img, Hb, Wb);
                 g.ctr = r.ctr;
                 g.ctr_stride = r.ctr_stride;
+                g.raster = 1;            // block of row r = (g0 + r, row counter, h): computed, not loaded
+                g.raster_img0 = g0[l];
+                g.raster_h = h;
                 if (!crc) crc = run_ctx(m, w, g, true, m->cap);
                 r.blocks = blocks;
                 r.ts = m->prof.active ? m->prof.take() : nullptr;

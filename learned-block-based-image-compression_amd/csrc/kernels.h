@@ -45,6 +45,8 @@ struct GemmArgs {
     const int4* blocks;      // per block (img, v, h, 0); row r belongs to block r / P
     const int* ctr;          // optional device counter: blocks += *ctr * ctr_stride (graph replays per row)
     int ctr_stride;
+    int raster;              // decoder raster step (needs ctr): the block of row r is (raster_img0 + r / P,
+    int raster_img0, raster_h;   // *ctr, raster_h), computed instead of loaded from `blocks`
     unsigned long long* ts;  // optional timing slot {max(~start), max(end)} in s_memrealtime ticks (100 MHz)
     const float* W;
     int NB16;                // N padded / 16

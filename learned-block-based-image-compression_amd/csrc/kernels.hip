@@ -73,10 +73,19 @@ __device__ __forceinline__ float std_cum(float x) {
     return 0.5f * erfcf(-0.70710677f * x);
 }
 
+// Block (img, v, h) of A-row block m: from the block list, or computed for a decoder raster step
+// (GemmArgs::raster: img = img0 + m, v = the graph's row counter, h fixed), which saves the kernel one
+// dependent global load before its first activation load.
+struct BlkSrc {
+    const int4* p;
+    int raster, img0, v, h;
+    __device__ __forceinline__ int4 at(int m) const { return raster ? make_int4(img0 + m, v, h, 0) : p[m]; }
+};
+
 // Output element (row, col) of a GEMM from its slice-ordered sum v: bias + the layer's epilogue.  Shared by
 // both GEMM kernels so that they compute bit-identical values.
 // bcol = bias[col]; xv = the GDN input x[row][col] (GDN / IGDN only), both loaded by the caller.
-__device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const int4* blocks, float bcol,
+__device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const BlkSrc& blocks, float bcol,
                                          float xv) {
     switch (g.epi) {
         case EPI_BIAS:
@@ -93,7 +102,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
                     dy = p == q ? g.pos_dy[q] : dy;
                     dx = p == q ? g.pos_dx[q] : dx;
                 }
-                const int4 b = blocks[m];
+                const int4 b = blocks.at(m);
                 const int vv = b.y + dy, hh = b.z + dx;
                 if (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb) o = 0.f;
             }
@@ -115,7 +124,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             const int sym = (int)rintf(d);               // torch.round: half to even
             const float yq = (float)sym + mean;
             g.out[(long)row * g.ldo + col] = yq;
-            const int4 b = blocks[row];
+            const int4 b = blocks.at(row);
             const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
             g.sym[pos] = sym;
             g.idx[pos] = g.table ? scale_index(scale, g.table) : 0;   // no table: forward()/validation before update()
@@ -133,13 +142,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             break;
         }
         case EPI_SCATTER: {   // output row of block (img, v, h) -> out[img][v][h][col] (forward()'s xhat)
-            const int4 b = blocks[row];
+            const int4 b = blocks.at(row);
             g.out[((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col] = v + bcol;
             break;
         }
         case EPI_CLAMPZ: {
             const float t = fminf(fmaxf(v + bcol, -0.5f), 0.5f);
-            const int4 b = blocks[row];
+            const int4 b = blocks.at(row);
             g.geo.zpad[((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col] = t;
             break;
         }
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         const int col = n0 + (sj % NS) * 16 + (l & 15);
         if (row >= g.M || col >= g.N) continue;
         const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-        epilogue(g, v, row, col, blocks, g.bias[col], gdn ? g.gx[(long)row * g.ldx + col] : 0.f);
+        epilogue(g, v, row, col, BlkSrc{blocks, 0, 0, 0, 0}, g.bias[col], gdn ? g.gx[(long)row * g.ldx + col] : 0.f);
     }
     PHASE(4);
     stamp_end(g.ts);
@@ -330,7 +339,8 @@ struct SBlk {
     int4 b;
 };
 
-__device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, const int4* blocks) {
+template <bool RASTER>
+__device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, const BlkSrc& blocks) {
     SBlk s;
     s.r = min(m0 + (lane & 15), g.M - 1);
     int m = s.r;
@@ -344,7 +354,8 @@ __device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, c
             s.dx = p == q ? g.pos_dx[q] : s.dx;
         }
     }
-    s.b = blocks[m];     // unconditional (a branch here costs a full vmcnt drain); unused by dense-only GEMMs
+    if constexpr (RASTER) s.b = make_int4(blocks.img0 + m, blocks.v, blocks.h, 0);
+    else s.b = blocks.p[m];   // unconditional (a branch here costs a full vmcnt drain); unused by dense-only GEMMs
     return s;
 }
 
@@ -382,14 +393,14 @@ __device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
 // differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
 // selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
-template <int L>
-__device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const int4* blocks,
+template <int L, bool RASTER>
+__device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const BlkSrc& blocks,
                                           f4 acc) {
     constexpr int LL = L + 1;
     const int nkb = g.K >> 4;
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     f4 w[LL], a[LL];
-    const SBlk bk = small_blk(g, m0, lane, blocks);      // issued first: the A addresses wait for it
+    const SBlk bk = small_blk<RASTER>(g, m0, lane, blocks);   // issued first: the A addresses wait for it
 #pragma unroll
     for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
     SRow rw;
@@ -414,7 +425,7 @@ __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int
 }
 
 // L = (K/16) / 8 k-blocks per slice (each slice L or L+1); L > 12: chunks of 12
-template <int L>
+template <int L, bool RASTER>
 __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256];
     const int lane = threadIdx.x & 63;
@@ -431,18 +442,20 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
 
     const int nkb = g.K >> 4;
     const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
-    const int4* blocks = g.blocks;
+    BlkSrc blocks{g.blocks, RASTER ? 1 : 0, g.raster_img0, 0, g.raster_h};
     if (g.need_blocks && g.ctr) {
         // scalar load: stays out of the vector-memory counter, so no weight load waits behind it
         int c;
         asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c) : "s"(g.ctr) : "memory");
-        blocks += (long)c * g.ctr_stride;
+        if constexpr (RASTER) blocks.v = c;
+        else blocks.p += (long)c * g.ctr_stride;
     }
     f4 acc = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (L <= 12) {
-        acc = small_slice<L>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
+        acc = small_slice<L, RASTER>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
     } else {
-        for (int c0 = kb0; c0 < kb1; c0 += 12) acc = small_slice<11>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
+        for (int c0 = kb0; c0 < kb1; c0 += 12)
+            acc = small_slice<11, RASTER>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
     }
     PHASE(3);
 #pragma unroll
@@ -505,12 +518,20 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
+        const bool raster = g.raster && g.ctr && g.need_blocks;
+        if (g.raster && !g.ctr) return set_error(LBC_E_ARG, "raster GEMM needs the row counter");
         switch ((g.K >> 4) / KSPLIT) {
-#define LBIC_L(L) case L: hipLaunchKernelGGL(k_gemm_s<L>, grid, dim3(512), 0, s, g); break;
+#define LBIC_L(L)                                                                                  \
+    case L:                                                                                        \
+        if (raster) hipLaunchKernelGGL((k_gemm_s<L, true>), grid, dim3(512), 0, s, g);             \
+        else hipLaunchKernelGGL((k_gemm_s<L, false>), grid, dim3(512), 0, s, g);                   \
+        break;
             LBIC_L(0) LBIC_L(1) LBIC_L(2) LBIC_L(3) LBIC_L(4) LBIC_L(5) LBIC_L(6)
             LBIC_L(7) LBIC_L(8) LBIC_L(9) LBIC_L(10) LBIC_L(11) LBIC_L(12)
 #undef LBIC_L
-            default: hipLaunchKernelGGL(k_gemm_s<13>, grid, dim3(512), 0, s, g);
+            default:
+                if (raster) hipLaunchKernelGGL((k_gemm_s<13, true>), grid, dim3(512), 0, s, g);
+                else hipLaunchKernelGGL((k_gemm_s<13, false>), grid, dim3(512), 0, s, g);
         }
         return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
     }
