@@ -84,7 +84,7 @@ struct Prof {
         return slots + kSlotU64 * ((size_t)range * kSlotsPerRange + next++);
     }
 };
-static const char* kKernelNames[] = {"k_gemm_s", "k_gemm<64,32,4>", "k_rans_decode", "k_copy_interior"};
+static const char* kKernelNames[] = {"k_gemm_s", "k_gemm", "k_rans_decode", "k_copy_interior"};
 static thread_local Prof* g_prof = nullptr;
 
 struct HostT {

@@ -45,6 +45,7 @@ struct GemmArgs {
     const int4* blocks;      // per block (img, v, h, 0); row r belongs to block r / P
     const int* ctr;          // optional device counter: blocks += *ctr * ctr_stride (graph replays per row)
     int ctr_stride;
+    int swz;                 // k_gemm: XCD-aware tile order (set by the launcher)
     int raster;              // decoder raster step (needs ctr): the block of row r is (raster_img0 + r / P,
     int raster_img0, raster_h;   // *ctr, raster_h), computed instead of loaded from `blocks`
     unsigned long long* ts;  // optional timing slot {max(~start), max(end)} in s_memrealtime ticks (100 MHz)
@@ -96,7 +97,7 @@ struct RansArgs {
     int streams_per_img;     // 1: one stream per image (reference format); Hb: one per block row (sub-stream format)
 };
 
-int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = <16,16,8>, 1 = <64,32,4>
+int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s);

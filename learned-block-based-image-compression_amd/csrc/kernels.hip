@@ -222,7 +222,14 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) float red[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: keeps the k-loop scalar
-    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+    // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin over the 8 XCDs,
+    // so XCD (bid % 8) gets a contiguous run of row-major tiles and its L2 serves their shared A rows
+    int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    if (g.swz) {
+        const int full = (gridDim.x * gridDim.y) & ~7;
+        if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    }
+    const int n0 = (bid % gridDim.x) * BN, m0 = (bid / gridDim.x) * BM;
     const int q4 = (lane >> 4) * 4;
 
     stamp_start(g.ts);
@@ -474,6 +481,22 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     stamp_end(g.ts);
 }
 
+static int enc_swz() {   // LBIC_ENC_SWZ=0 disables the XCD-aware tile order (A/B experiments)
+    const char* e = getenv("LBIC_ENC_SWZ");
+    return e ? atoi(e) : 1;
+}
+static const int g_enc_swz = enc_swz();
+static int enc_cfg() {
+    const char* e = getenv("LBIC_ENC_CFG");
+    return e ? atoi(e) : 0;
+}
+static const int g_enc_cfg = enc_cfg();
+static int small_max() {   // LBIC_SMALL_MAX: largest M for the small-M kernel (experiments)
+    const char* e = getenv("LBIC_SMALL_MAX");
+    return e ? atoi(e) : 64;
+}
+static const int g_small_max = small_max();
+
 template <int BM, int BN, int NW, int CH>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
@@ -485,7 +508,9 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
         attr = true;
     }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH>), grid, dim3(NW * 64), lds, s, g);
+    GemmArgs gs = g;
+    gs.swz = g_enc_swz;
+    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH>), grid, dim3(NW * 64), lds, s, gs);
     return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm launch failed");
 }
 
@@ -515,7 +540,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         g.seg[t] = g.seg[0];
         g.seg[t].k0 = g.seg[t].k1 = 1 << 30;
     }
-    if (g.M <= 64) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
+    if (g.M <= g_small_max) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
         const bool raster = g.raster && g.ctr && g.need_blocks;
@@ -536,7 +561,16 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
     }
     if (cfg_id) *cfg_id = 1;
-    return launch_cfg<64, 32, 4, 2>(g, s);
+    // Encoder wavefront steps (M = 32 images x up to 48 blocks): many small tiles beat few large ones
+    // (measured encode time per 32-frame batch: 64x32 / 4 waves 149 ms, 32x32 121, 16x32 / 4 waves 114,
+    // 16x32 / 8 waves 112): the per-tile K loop is latency-bound, so the step wants more workgroups.
+    // LBIC_ENC_CFG selects the earlier shapes for A/B runs (results are identical for every shape).
+    switch (g_enc_cfg) {
+        case 1: return launch_cfg<64, 32, 4, 2>(g, s);
+        case 2: return launch_cfg<16, 32, 4, 2>(g, s);
+        case 3: return launch_cfg<32, 32, 8, 2>(g, s);
+        default: return launch_cfg<16, 32, 8, 2>(g, s);
+    }
 }
 
 // ----------------------------------------------------------------------------------------- rANS decode
