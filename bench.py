@@ -5,10 +5,10 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU.  One step = the reference's timed region of eval_model
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
-GPU rANS decode).  Batches are software-pipelined (default --depth 2): two batch decodes are in flight
-(latency-bound raster chains, each on its own codec handle and HIP stream, few CUs busy) while the next
-batches are compressed and entropy coded on a third handle/stream; the timed region holds exactly `steps`
-compressions and `steps` decompressions.  The one-decode-in-flight pipeline and the non-overlapped serial
+GPU rANS decode).  Batches are software-pipelined: 3-4 batch decodes are in flight (latency-bound raster
+chains, each on its own codec handle and HIP stream, few CUs busy each) while the next batches are
+compressed and entropy coded on another handle/stream; the timed region holds exactly `steps` compressions
+and `steps` decompressions of 32-frame batches.  The one-decode-in-flight pipeline and the non-overlapped serial
 schedule are reported beside it ("two_stage_schedule", "serial_schedule"; --depth 1 / --serial select them).
 Inputs are resident in HBM when the timed region starts.  Weights are the seeded
 synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
@@ -84,7 +84,7 @@ def cpu_baseline(arch, sd, H, W, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
@@ -93,9 +93,11 @@ def main():
     ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
-    ap.add_argument("--depth", type=int, default=2,
-                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; 3+ serialises on "
-                         "ROCm 7.2's 4 hardware queues per process)")
+    ap.add_argument("--depth", type=int, default=0,
+                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; default: 4 when "
+                         "--steps is a multiple of 4, else 3 -- the decode of a batch is a latency-bound chain, "
+                         "and 3-4 of them side by side fill the GPU; whole rounds of decodes keep the timed "
+                         "region free of a partly filled last round)")
     ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
                     help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
@@ -136,7 +138,7 @@ def main():
     # codec handles with their own workspaces and reconstruction buffers: one encoder side and `depth`
     # decoder sides of the pipeline, each on its own HIP stream (created back to back so they land on
     # distinct hardware queues)
-    depth = 0 if args.serial else args.depth
+    depth = 0 if args.serial else (args.depth or (4 if args.steps % 4 == 0 else 3))
     enc_model = make_model()
     dec_models = [make_model() for _ in range(max(depth, 1))]
     if depth and args.enc_lds_floor:

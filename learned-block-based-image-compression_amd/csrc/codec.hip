@@ -308,7 +308,8 @@ int prepare_device(lbc_model* m) {
     if (!m->ev[0]) {
         for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
         for (auto& e : m->lev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (auto& st : m->lstream) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        // (lane streams are created only when a decode uses several lanes: every stream a process creates
+        // takes a turn on its few hardware queues, and two busy streams on one queue serialise)
         HIPCHK(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
     }
     if (m->tabs_dirty) {
@@ -945,14 +946,21 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
         m->dec_key = key;
     }
     HIPCHK(hipMemsetAsync(m->ctr.p, 0, kLanes * sizeof(int), s));
-    HIPCHK(hipEventRecord(m->lev[kLanes], s));
-    for (int l = 0; l < G; ++l) HIPCHK(hipStreamWaitEvent(m->lstream[l], m->lev[kLanes], 0));
-    for (int v = 0; v < Hb; ++v)
-        for (int l = 0; l < G; ++l) HIPCHK(hipGraphLaunch(m->dec_exec[l], m->lstream[l]));
-    for (int l = 0; l < G; ++l) m->prof.replays[1 + l] += Hb;
-    for (int l = 0; l < G; ++l) {
-        HIPCHK(hipEventRecord(m->lev[l], m->lstream[l]));
-        HIPCHK(hipStreamWaitEvent(s, m->lev[l], 0));
+    if (G == 1) {      // one lane: the row graphs run on the caller's stream
+        for (int v = 0; v < Hb; ++v) HIPCHK(hipGraphLaunch(m->dec_exec[0], s));
+        m->prof.replays[1] += Hb;
+    } else {
+        for (int l = 0; l < G; ++l)
+            if (!m->lstream[l]) HIPCHK(hipStreamCreateWithFlags(&m->lstream[l], hipStreamNonBlocking));
+        HIPCHK(hipEventRecord(m->lev[kLanes], s));
+        for (int l = 0; l < G; ++l) HIPCHK(hipStreamWaitEvent(m->lstream[l], m->lev[kLanes], 0));
+        for (int v = 0; v < Hb; ++v)
+            for (int l = 0; l < G; ++l) HIPCHK(hipGraphLaunch(m->dec_exec[l], m->lstream[l]));
+        for (int l = 0; l < G; ++l) m->prof.replays[1 + l] += Hb;
+        for (int l = 0; l < G; ++l) {
+            HIPCHK(hipEventRecord(m->lev[l], m->lstream[l]));
+            HIPCHK(hipStreamWaitEvent(s, m->lev[l], 0));
+        }
     }
     m->prof.active = false;
     g_prof = nullptr;
