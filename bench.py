@@ -94,10 +94,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
     ap.add_argument("--depth", type=int, default=0,
-                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; default: 4 when "
-                         "--steps is a multiple of 4, else 3 -- the decode of a batch is a latency-bound chain, "
-                         "and 3-4 of them side by side fill the GPU; whole rounds of decodes keep the timed "
-                         "region free of a partly filled last round)")
+                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; default 3: the decode of "
+                         "a batch is a latency-bound chain, and 3 of them side by side plus the encoder use the "
+                         "process's 4 hardware queues; --steps a multiple of the depth keeps the timed region "
+                         "free of a partly filled last round of decodes)")
     ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
                     help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
@@ -138,7 +138,7 @@ def main():
     # codec handles with their own workspaces and reconstruction buffers: one encoder side and `depth`
     # decoder sides of the pipeline, each on its own HIP stream (created back to back so they land on
     # distinct hardware queues)
-    depth = 0 if args.serial else (args.depth or (4 if args.steps % 4 == 0 else 3))
+    depth = 0 if args.serial else (args.depth or 3)
     enc_model = make_model()
     dec_models = [make_model() for _ in range(max(depth, 1))]
     if depth and args.enc_lds_floor:
