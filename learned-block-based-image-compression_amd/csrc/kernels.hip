@@ -400,10 +400,10 @@ __device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
 // differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
 // selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
-template <int L, bool RASTER>
+template <int L, bool RASTER, bool EXACT = false>
 __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const BlkSrc& blocks,
                                           f4 acc) {
-    constexpr int LL = L + 1;
+    constexpr int LL = EXACT ? L : L + 1;     // EXACT: every slice has exactly L k-blocks (K/16 divisible by 8)
     const int nkb = g.K >> 4;
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     f4 w[LL], a[LL];
@@ -432,7 +432,7 @@ __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int
 }
 
 // L = (K/16) / 8 k-blocks per slice (each slice L or L+1); L > 12: chunks of 12
-template <int L, bool RASTER>
+template <int L, bool RASTER, bool EXACT>
 __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256];
     const int lane = threadIdx.x & 63;
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     }
     f4 acc = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (L <= 12) {
-        acc = small_slice<L, RASTER>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
+        acc = small_slice<L, RASTER, EXACT>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
     } else {
         for (int c0 = kb0; c0 < kb1; c0 += 12)
             acc = small_slice<11, RASTER>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
@@ -496,6 +496,11 @@ static int small_max() {   // LBIC_SMALL_MAX: largest M for the small-M kernel (
     return e ? atoi(e) : 64;
 }
 static const int g_small_max = small_max();
+static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B experiments)
+    const char* e = getenv("LBIC_EXACT");
+    return e ? atoi(e) : 1;
+}
+static const int g_exact = exact_on();
 
 template <int BM, int BN, int NW, int CH>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
@@ -545,18 +550,31 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
         const bool raster = g.raster && g.ctr && g.need_blocks;
         if (g.raster && !g.ctr) return set_error(LBC_E_ARG, "raster GEMM needs the row counter");
+        // every slice exactly L k-blocks: no (L+1)-th block to load (loads are what a launch waits for)
+        const bool exact = ((g.K >> 4) % KSPLIT) == 0 && g_exact;
+        const int sel = (raster ? 1 : 0) + (exact ? 2 : 0);
         switch ((g.K >> 4) / KSPLIT) {
+#define LBIC_V(L, R, E) hipLaunchKernelGGL((k_gemm_s<L, R, E>), grid, dim3(512), 0, s, g)
 #define LBIC_L(L)                                                                                  \
     case L:                                                                                        \
-        if (raster) hipLaunchKernelGGL((k_gemm_s<L, true>), grid, dim3(512), 0, s, g);             \
-        else hipLaunchKernelGGL((k_gemm_s<L, false>), grid, dim3(512), 0, s, g);                   \
+        switch (sel) {                                                                             \
+            case 0: LBIC_V(L, false, false); break;                                                \
+            case 1: LBIC_V(L, true, false); break;                                                 \
+            case 2: LBIC_V(L, false, true); break;                                                 \
+            default: LBIC_V(L, true, true); break;                                                 \
+        }                                                                                          \
         break;
-            LBIC_L(0) LBIC_L(1) LBIC_L(2) LBIC_L(3) LBIC_L(4) LBIC_L(5) LBIC_L(6)
+            case 0:
+                if (raster) LBIC_V(0, true, false);
+                else LBIC_V(0, false, false);
+                break;
+            LBIC_L(1) LBIC_L(2) LBIC_L(3) LBIC_L(4) LBIC_L(5) LBIC_L(6)
             LBIC_L(7) LBIC_L(8) LBIC_L(9) LBIC_L(10) LBIC_L(11) LBIC_L(12)
 #undef LBIC_L
             default:
-                if (raster) hipLaunchKernelGGL((k_gemm_s<13, true>), grid, dim3(512), 0, s, g);
-                else hipLaunchKernelGGL((k_gemm_s<13, false>), grid, dim3(512), 0, s, g);
+                if (raster) LBIC_V(13, true, false);
+                else LBIC_V(13, false, false);
+#undef LBIC_V
         }
         return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
     }
