@@ -5,11 +5,14 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU.  One step = the reference's timed region of eval_model
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
-GPU rANS decode).  Batches are software-pipelined: 3-4 batch decodes are in flight (latency-bound raster
-chains, each on its own codec handle and HIP stream, few CUs busy each) while the next batches are
-compressed and entropy coded on another handle/stream; the timed region holds exactly `steps` compressions
-and `steps` decompressions of 32-frame batches.  The one-decode-in-flight pipeline and the non-overlapped serial
-schedule are reported beside it ("two_stage_schedule", "serial_schedule"; --depth 1 / --serial select them).
+GPU rANS decode).  Batches are software-pipelined: the raster decode is a chain of Hb*Wb latency-bound
+steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 8)
+queued batches in one raster pass, and 2 such passes run side by side (own codec handle + HIP stream each),
+while the next batches are compressed on the GPU (another handle/stream) and entropy coded on host threads.
+The timed region holds exactly `steps` compressions and `steps` decompressions of 32-frame batches, every
+batch fully encoded and fully decoded (bit-exactness of the last one is checked).  The one-decode-in-flight
+pipeline and the non-overlapped serial schedule are reported beside it ("two_stage_schedule",
+"serial_schedule"; --depth 1 --gang 1 / --serial select them).
 Inputs are resident in HBM when the timed region starts.  Weights are the seeded
 synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
 checkpoints offline).
@@ -84,7 +87,7 @@ def cpu_baseline(arch, sd, H, W, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
@@ -94,10 +97,16 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
     ap.add_argument("--depth", type=int, default=0,
-                    help="batch decodes in flight beside the encoder (1 = two-stage pipeline; default 3: the decode of "
-                         "a batch is a latency-bound chain, and 3 of them side by side plus the encoder use the "
-                         "process's 4 hardware queues; --steps a multiple of the depth keeps the timed region "
-                         "free of a partly filled last round of decodes)")
+                    help="decoder handles in flight beside the encoder (1 = two-stage pipeline; default 2).  The "
+                         "raster decode is a latency-bound chain: more rows per step (--gang) and two chains side by "
+                         "side fill the GPU; the process's 4 hardware queues hold the encoder, 2 decoders and the "
+                         "copies.  --steps a multiple of depth x gang keeps the timed region free of a partly "
+                         "filled last round of decodes")
+    ap.add_argument("--gang", type=int, default=8,
+                    help="batches decoded together by one decoder handle (one raster pass over gang x batch streams: "
+                         "a raster step's latency barely grows with its rows)")
+    ap.add_argument("--enc-gang", type=int, default=1,
+                    help="batches compressed together in one wavefront pass (steps must be a multiple)")
     ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
                     help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
@@ -138,7 +147,7 @@ def main():
     # codec handles with their own workspaces and reconstruction buffers: one encoder side and `depth`
     # decoder sides of the pipeline, each on its own HIP stream (created back to back so they land on
     # distinct hardware queues)
-    depth = 0 if args.serial else (args.depth or 3)
+    depth = 0 if args.serial else (args.depth or 2)
     enc_model = make_model()
     dec_models = [make_model() for _ in range(max(depth, 1))]
     if depth and args.enc_lds_floor:
@@ -166,19 +175,34 @@ def main():
             v = float(t.item())
         return v
 
-    def encode_side(fmt, ph):
-        """compress (GPU) + host rANS of one batch on the encoder stream -> (result, streams)"""
+    def compress_side(ph, egang=1):
+        """compress (GPU) on the encoder stream: one batch, or `egang` batches in one wavefront pass -> a list of
+        per-batch results"""
         t0 = time.perf_counter()
         with torch.cuda.stream(s_enc):
-            r = enc_model.compress_batch(xb)
+            r = enc_model.compress_batch(xb if egang == 1 else xb_gang)
+            # symbols/indexes for the host rANS: DMA into page-locked buffers (torch's caching host allocator)
+            # on the encoder's stream, ahead of the next batch's compress
+            for k in ("symbols", "indexes"):
+                h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
+                h.copy_(r[k], non_blocking=True)
+                r[k] = h
             s_enc.synchronize()
-            t1 = time.perf_counter()
-            st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
-        t2 = time.perf_counter()
         with plock:
-            ph["encode"] += t1 - t0
-            ph["entropy"] += t2 - t1
-        return r, st
+            ph["encode"] += time.perf_counter() - t0
+        return [{k: (v[e * n:(e + 1) * n] if v is not None else None) for k, v in r.items()} for e in range(egang)]
+
+    def entropy_side(r, fmt, ph):
+        """host rANS of a compressed batch (reference format: one stream per image) -> streams"""
+        t0 = time.perf_counter()
+        st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)   # host tensors
+        with plock:
+            ph["entropy"] += time.perf_counter() - t0
+        return st
+
+    def encode_side(fmt, ph):
+        r = compress_side(ph)[0]
+        return r, entropy_side(r, fmt, ph)
 
     def decode_side(i, st, fmt, ph):
         t0 = time.perf_counter()
@@ -198,24 +222,29 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    def run(fmt, steps, warmup, depth, label, prof=False):
+    def run(fmt, steps, warmup, depth, label, prof=False, gang=1, egang=1):
         """`steps` timed batches.  depth 0: encode, entropy, decode one after another.  depth D >= 1: a software
-        pipeline -- D decoder handles (own streams, helper threads; ctypes drops the GIL) decode batches in
-        order from a queue of at most D encoded batches, while this thread compresses and entropy codes the
-        next ones.  The timed region holds exactly `steps` encodes and `steps` decodes: the pipeline is primed
-        with D encodes and drained with D decodes outside it (its steady state)."""
+        pipeline -- D decoder handles (own streams, helper threads; ctypes drops the GIL) decode `gang` batches
+        per raster pass from a queue of at most D*gang encoded batches, while this thread compresses the next
+        batches on the GPU and a helper thread entropy codes them on the host.  The timed region holds exactly
+        `steps` encodes and `steps` decodes: the pipeline is primed with D*gang encodes and drained with D*gang
+        decodes outside it (its steady state)."""
         ph = dict(encode=0.0, entropy=0.0, decode=0.0)
         scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
         for i in range(warmup):
             for d in range(len(dec_models)):          # every decoder handle builds its graphs
                 r, st = encode_side(fmt, scratch)
-                decode_side(d, st, fmt, scratch)
+                decode_side(d, list(st) * gang, fmt, scratch)
+            if egang > 1:                             # and the encoder its ganged graph
+                compress_side(scratch, egang)
             log(f"[rank {rank}] {label} warmup {i + 1}/{warmup} done")
-        if prof:      # launch counts cover the timed region only (same sampling period: graphs are kept)
-            for m_ in handles:
-                m_.profile_begin(args.sample_every)
+        def prof_begin():   # launch counts cover the timed region only (same sampling period: graphs are kept)
+            if prof:
+                for m_ in handles:
+                    m_.profile_begin(args.sample_every)
         last = []
         if depth == 0:
+            prof_begin()
             barrier()
             t0 = time.perf_counter()
             for i in range(steps):
@@ -226,64 +255,98 @@ def main():
             dt = max_over_ranks(time.perf_counter() - t0)
             return dt, ph, (last[-1] if last else None), collect_stats() if prof else None
         import queue
-        pending = [encode_side(fmt, scratch) for _ in range(depth)]      # prime
-        q = queue.Queue(maxsize=depth)
-        done = []
+        primed = []                                 # prime (with the encoder's own pass shape: graphs are kept)
+        while len(primed) < depth * gang:
+            primed += [(r_, entropy_side(r_, fmt, scratch)) for r_ in compress_side(scratch, egang)]
+        del primed[depth * gang:]
+        prof_begin()
+        q = queue.Queue(maxsize=depth * gang)      # encoded batches waiting for a decoder
+        eq = queue.Queue(maxsize=1)                # compressed batches waiting for the host rANS
+        done, pending = [], []
+        glock = threading.Lock()
 
         def decoder(i):
             while True:
-                item = q.get()
-                if item is None:
+                items, end = [], False
+                with glock:                       # one decoder gathers its whole gang
+                    while len(items) < gang:      # gang decode: up to `gang` queued batches in one raster pass
+                        item = q.get()
+                        if item is None:
+                            end = True
+                            break
+                        items.append(item)
+                if items:
+                    z_ = decode_side(i, [b for _, (_, st_) in items for b in st_], fmt, ph)
+                    with plock:
+                        for k, (j, (r_, st_)) in enumerate(items):
+                            done.append((j, r_, st_, z_[k * n:(k + 1) * n]))
+                    log(f"[rank {rank}] {label} batches {[j for j, _ in items]} decoded (decoder {i}): "
+                        f"{time.perf_counter() - t0:.2f} s")
+                if end:
+                    q.put(None)                   # pass the end mark on to the other decoders
                     return
-                j, (r_, st_) = item
-                z_ = decode_side(i, st_, fmt, ph)
-                with plock:
-                    done.append((j, r_, st_, z_))
-                log(f"[rank {rank}] {label} batch {j} decoded (decoder {i}): {time.perf_counter() - t0:.2f} s")
 
-        fed = [0]
-
-        def feed():
-            while pending and fed[0] < steps:
-                q.put((fed[0], pending.pop(0)))
-                fed[0] += 1
+        def entropy_worker():
+            # host rANS of batch k beside the GPU compress of batch k+1 (this thread's pool drops the GIL);
+            # batches past `steps` are entropy coded inside the timed region but decoded after it (the drain)
+            while True:
+                item = eq.get()
+                if item is None:
+                    q.put(None)
+                    return
+                j0, rs_ = item
+                for e, r_ in enumerate(rs_):
+                    st_ = entropy_side(r_, fmt, ph)
+                    if j0 + e < steps:
+                        q.put((j0 + e, (r_, st_)))
+                    else:
+                        pending.append((r_, st_))
 
         ths = [threading.Thread(target=decoder, args=(i,)) for i in range(depth)]
+        eth = threading.Thread(target=entropy_worker)
         barrier()
         t0 = time.perf_counter()
         for th in ths:
             th.start()
-        feed()
-        for i in range(steps):
-            pending.append(encode_side(fmt, ph))
-            feed()
-        for _ in ths:
-            q.put(None)
+        for k, e in enumerate(primed[:steps]):
+            q.put((k, e))
+        pending.extend(primed[steps:])
+        eth.start()
+        for i in range(0, steps, egang):
+            eq.put((len(primed) + i, compress_side(ph, egang)))
+        eq.put(None)
+        eth.join()
         for th in ths:
             th.join()
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         ks = collect_stats() if prof else None
-        for k, (r_, st_) in enumerate(pending):                        # drain (outside the timed region)
-            decode_side(k % depth, st_, fmt, scratch)
+        for k in range(0, len(pending), gang):                         # drain (outside the timed region)
+            decode_side((k // gang) % depth, [b for _, st_ in pending[k:k + gang] for b in st_], fmt, scratch)
         j, r_, st_, z_ = max(done, key=lambda e: e[0])
         return dt, ph, (r_, st_, z_), ks
 
     # sampling is part of the captured graphs: enable it before the warmup builds them
     for m_ in handles:
         m_.profile_begin(args.sample_every)
-    run("reference", 0, args.warmup, 0, "warmup")
-    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, depth, "reference", prof=True)
+    gang = max(1, args.gang) if depth else 1
+    egang = max(1, args.enc_gang) if depth else 1
+    if args.steps % egang:
+        raise SystemExit("--steps must be a multiple of --enc-gang")
+    xb_gang = xb.repeat(egang, 1, 1, 1) if egang > 1 else None
+    run("reference", 0, args.warmup, 0, "warmup", gang=gang, egang=egang)
+    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, depth, "reference", prof=True, gang=gang,
+                                             egang=egang)
 
     def summary(dts, phs, k):
         return dict(value=round(world * n * H * W / (dts / k) / 1e6, 4), ms_per_step=round(dts / k * 1e3, 2),
                     steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in phs.items()})
     serial = two_stage = None
     if depth and args.serial_steps > 0:     # the same batches without the overlap, for reference
-        dts, phs, _, _ = run("reference", args.serial_steps, 0, 0, "serial")
+        dts, phs, _, _ = run("reference", args.serial_steps, 1 if gang * egang > 1 else 0, 0, "serial")
         serial = summary(dts, phs, args.serial_steps)
     if depth > 1 and args.serial_steps > 0:  # one decoder in flight
-        dts, phs, _, _ = run("reference", 2 * args.serial_steps, 0, 1, "two-stage")
+        dts, phs, _, _ = run("reference", 2 * args.serial_steps, 1 if gang * egang > 1 else 0, 1, "two-stage")
         two_stage = summary(dts, phs, 2 * args.serial_steps)
 
     # --- opt-in sub-stream format: same encoder, one rANS stream per block row, wavefront
@@ -377,10 +440,12 @@ def main():
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
                    "global_batch": n * world,
                    "schedule": "serial: encode, entropy, decode per batch" if depth == 0 else
-                   f"software pipeline: {depth} batch decode(s) in flight (one codec handle + HIP stream each) "
-                   "beside the compress + host rANS of the next batches (own handle + stream); each timed step = "
-                   f"one full encode and one full decode of a {n}-frame batch",
-                   "decode_batches_in_flight": depth},
+                   f"software pipeline: {depth} raster decode pass(es) in flight (one codec handle + HIP stream "
+                   f"each), each over {gang} queued batches, beside the GPU compress and host rANS of the next "
+                   f"batches (own handle + stream, host threads); each timed step = one full encode and one full "
+                   f"decode of a {n}-frame batch",
+                   "decode_passes_in_flight": depth, "batches_per_decode_pass": gang,
+                   "batches_per_encode_pass": egang},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"bpp": round(bpp, 5), "psnr_db": round(psnr, 3), "enc_dec_bit_exact": bit_exact},
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},

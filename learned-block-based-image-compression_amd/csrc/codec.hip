@@ -342,7 +342,7 @@ int prof_range_begin(Prof* p, int r, hipStream_t s) {
 // launch a GEMM; in a sampled step give it a timing slot and record its algorithmic work
 int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     Prof* p = g_prof;
-    if (p) p->per_replay[p->range][g0.M <= 64 ? 0 : 1] += 1;   // the class launch_gemm will pick
+    if (p) p->per_replay[p->range][gemm_class(g0)] += 1;   // the class launch_gemm will pick
     if (!p || !p->active) return launch_gemm(g0, s);
     GemmArgs g = g0;
     g.ts = p->take();

@@ -98,6 +98,7 @@ struct RansArgs {
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
+int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = k_gemm
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s);

@@ -496,6 +496,17 @@ static int small_max() {   // LBIC_SMALL_MAX: largest M for the small-M kernel (
     return e ? atoi(e) : 64;
 }
 static const int g_small_max = small_max();
+static int dec_small_max() {   // LBIC_DEC_SMALL_MAX: largest M for the small-M kernel in decoder raster steps
+    const char* e = getenv("LBIC_DEC_SMALL_MAX");
+    return e ? atoi(e) : 256;
+}
+static const int g_dec_small_max = dec_small_max();
+
+// 0 = k_gemm_s (latency-shaped, any M; the decoder's raster steps stay on it when several batches are decoded
+// together: a raster step's latency barely grows with its rows), 1 = k_gemm (the encoder's wavefront steps)
+int gemm_class(const GemmArgs& g) {
+    return (g.M <= g_small_max || (g.raster && g.M <= g_dec_small_max)) ? 0 : 1;
+}
 static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B experiments)
     const char* e = getenv("LBIC_EXACT");
     return e ? atoi(e) : 1;
@@ -545,7 +556,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         g.seg[t] = g.seg[0];
         g.seg[t].k0 = g.seg[t].k1 = 1 << 30;
     }
-    if (g.M <= g_small_max) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
+    if (gemm_class(g) == 0) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
         const bool raster = g.raster && g.ctr && g.need_blocks;

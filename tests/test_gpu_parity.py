@@ -305,3 +305,24 @@ def test_validate_recu_reco_matches_reference(name):
     if arch.KS[1] == 1:
         r = m.compress_batch(x.permute(0, 2, 3, 1).contiguous(), want_bits=True)
         assert torch.equal(r["zhat"].permute(0, 3, 1, 2), zhat)
+
+
+@pytest.mark.parametrize("name,n_img", [("tiny_ks3111", 83), ("tiny_ks3311", 150), ("b8_lowrate_2rows", 96)])
+def test_gang_decode_many_rows(name, n_img):
+    """Decoder raster steps with n_img > 64 rows (several batches decoded in one raster pass, as bench.py's
+    pipeline does) stay on the latency-shaped kernel (LBIC_DEC_SMALL_MAX, default 256) and must reproduce the
+    encoder's reconstruction bit-exactly, also for row counts that are not a multiple of the 16-row tile."""
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    m = model_for(arch, int(g["weight_seed"]))
+    x0 = torch.from_numpy(g["x"])[None].cuda()
+    noise = torch.rand((n_img - 1,) + tuple(x0.shape[1:]), generator=torch.Generator().manual_seed(7)).cuda() - 0.5
+    x = torch.cat([x0, noise])
+    r = m.compress_batch(x)
+    assert np.array_equal(r["symbols"][0].cpu().numpy(), g["symbols"])
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    zdec = m.decompress_batch(streams, *g["x"].shape[:2])
+    assert torch.equal(zdec, r["zhat"]), "ganged decode differs from the encoder's reconstruction"
+    # and as two passes of the same handle with different row counts (graphs rebuilt per shape)
+    z2 = m.decompress_batch(streams[:17], *g["x"].shape[:2])
+    assert torch.equal(z2, r["zhat"][:17])
