@@ -6,9 +6,10 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
 GPU rANS decode).  Batches are software-pipelined: the raster decode is a chain of Hb*Wb latency-bound
-steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 8)
+steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 16)
 queued batches in one raster pass, and 2 such passes run side by side (own codec handle + HIP stream each),
-while the next batches are compressed on the GPU (another handle/stream) and entropy coded on host threads.
+while the next batches are compressed on the GPU (another handle/stream; `enc-gang` (default 4) batches of
+distinct frames per wavefront pass) and entropy coded on host threads.
 The timed region holds exactly `steps` compressions and `steps` decompressions of 32-frame batches, every
 batch fully encoded and fully decoded (bit-exactness of the last one is checked).  The one-decode-in-flight
 pipeline and the non-overlapped serial schedule are reported beside it ("two_stage_schedule",
@@ -102,13 +103,15 @@ def main():
                          "side fill the GPU; the process's 4 hardware queues hold the encoder, 2 decoders and the "
                          "copies.  --steps a multiple of depth x gang keeps the timed region free of a partly "
                          "filled last round of decodes")
-    ap.add_argument("--gang", type=int, default=8,
+    ap.add_argument("--gang", type=int, default=16,
                     help="batches decoded together by one decoder handle (one raster pass over gang x batch streams: "
                          "a raster step's latency barely grows with its rows)")
-    ap.add_argument("--enc-gang", type=int, default=1,
+    ap.add_argument("--enc-gang", type=int, default=4,
                     help="batches compressed together in one wavefront pass (steps must be a multiple)")
     ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
                     help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
+    ap.add_argument("--encode-only", type=int, default=0,
+                    help="profiling aid: run this many encoder passes (enc-gang batches each) and exit (no JSON line)")
     ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
     ap.add_argument("--substream-steps", type=int, default=2,
                     help="extra steps in the opt-in per-row sub-stream format, reported apart (0 = skip)")
@@ -158,9 +161,15 @@ def main():
     plock = threading.Lock()
 
     n = args.batch
-    frames = np.stack([image_to_blocks(np.random.default_rng(rank * n + k).integers(0, 256, (3, H, W), dtype=np.uint8)
-                                       .astype(np.float32) / 255.0 - 0.5, B) for k in range(n)])
-    xb = torch.from_numpy(frames).to(dev)
+    # an encoder pass over `egang` batches compresses egang x n distinct frames (batch e = frames e*n .. e*n+n-1)
+    egang = max(1, args.enc_gang) if depth else 1
+    if args.steps % egang:
+        raise SystemExit("--steps must be a multiple of --enc-gang")
+    frames = np.stack([image_to_blocks(np.random.default_rng(rank * n * egang + k).integers(0, 256, (3, H, W),
+                                                                                       dtype=np.uint8)
+                                       .astype(np.float32) / 255.0 - 0.5, B) for k in range(n * egang)])
+    xb_all = torch.from_numpy(frames).to(dev)
+    xb = xb_all[:n]
     del frames
 
     def barrier():
@@ -180,7 +189,7 @@ def main():
         per-batch results"""
         t0 = time.perf_counter()
         with torch.cuda.stream(s_enc):
-            r = enc_model.compress_batch(xb if egang == 1 else xb_gang)
+            r = enc_model.compress_batch(xb if egang == 1 else xb_all)
             # symbols/indexes for the host rANS: DMA into page-locked buffers (torch's caching host allocator)
             # on the encoder's stream, ahead of the next batch's compress
             for k in ("symbols", "indexes"):
@@ -190,7 +199,8 @@ def main():
             s_enc.synchronize()
         with plock:
             ph["encode"] += time.perf_counter() - t0
-        return [{k: (v[e * n:(e + 1) * n] if v is not None else None) for k, v in r.items()} for e in range(egang)]
+        return [dict({k: (v[e * n:(e + 1) * n] if v is not None else None) for k, v in r.items()}, frames=e)
+                for e in range(egang)]
 
     def entropy_side(r, fmt, ph):
         """host rANS of a compressed batch (reference format: one stream per image) -> streams"""
@@ -330,10 +340,11 @@ def main():
     for m_ in handles:
         m_.profile_begin(args.sample_every)
     gang = max(1, args.gang) if depth else 1
-    egang = max(1, args.enc_gang) if depth else 1
-    if args.steps % egang:
-        raise SystemExit("--steps must be a multiple of --enc-gang")
-    xb_gang = xb.repeat(egang, 1, 1, 1) if egang > 1 else None
+    if args.encode_only:      # e.g. rocprofv3 --pmc on the encoder's real launch shapes (tools/gpu_profile.sh)
+        for i in range(args.encode_only):
+            compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), egang)
+            log(f"[rank {rank}] encoder pass {i + 1}/{args.encode_only} ({egang} batches) done")
+        return
     run("reference", 0, args.warmup, 0, "warmup", gang=gang, egang=egang)
     dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, depth, "reference", prof=True, gang=gang,
                                              egang=egang)
@@ -363,7 +374,8 @@ def main():
 
     # --- quality / consistency of the last decoded batch (outside the timed region)
     bit_exact = bool(torch.equal(z, r["zhat"]))
-    sse = ((z - xb) ** 2).double().sum(dim=(1, 2, 3))
+    xq = xb_all[r["frames"] * n:(r["frames"] + 1) * n]      # the frames of that batch
+    sse = ((z - xq) ** 2).double().sum(dim=(1, 2, 3))
     rec = torch.stack([torch.tensor([float(len(s)) for s in streams], dtype=torch.float64, device=dev), sse,
                        torch.full((n,), float(H * W * 3), dtype=torch.float64, device=dev)], dim=1)
     if dist:

@@ -498,7 +498,7 @@ static int small_max() {   // LBIC_SMALL_MAX: largest M for the small-M kernel (
 static const int g_small_max = small_max();
 static int dec_small_max() {   // LBIC_DEC_SMALL_MAX: largest M for the small-M kernel in decoder raster steps
     const char* e = getenv("LBIC_DEC_SMALL_MAX");
-    return e ? atoi(e) : 256;
+    return e ? atoi(e) : 1024;   // ganged raster passes of up to 32 batches of 32 images
 }
 static const int g_dec_small_max = dec_small_max();
 

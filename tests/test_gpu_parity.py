@@ -310,7 +310,7 @@ def test_validate_recu_reco_matches_reference(name):
 @pytest.mark.parametrize("name,n_img", [("tiny_ks3111", 83), ("tiny_ks3311", 150), ("b8_lowrate_2rows", 96)])
 def test_gang_decode_many_rows(name, n_img):
     """Decoder raster steps with n_img > 64 rows (several batches decoded in one raster pass, as bench.py's
-    pipeline does) stay on the latency-shaped kernel (LBIC_DEC_SMALL_MAX, default 256) and must reproduce the
+    pipeline does) stay on the latency-shaped kernel (LBIC_DEC_SMALL_MAX, default 1024) and must reproduce the
     encoder's reconstruction bit-exactly, also for row counts that are not a multiple of the 16-row tile."""
     g = load_golden("loop_" + name)
     arch = golden_arch(g)
