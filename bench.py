@@ -6,7 +6,7 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 (agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
 rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
 GPU rANS decode).  Batches are software-pipelined: the raster decode is a chain of Hb*Wb latency-bound
-steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 16)
+steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 32)
 queued batches in one raster pass, and 2 such passes run side by side (own codec handle + HIP stream each),
 while the next batches are compressed on the GPU (another handle/stream; `enc-gang` (default 4) batches of
 distinct frames per wavefront pass) and entropy coded on host threads.
@@ -88,7 +88,7 @@ def cpu_baseline(arch, sd, H, W, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
@@ -103,7 +103,7 @@ def main():
                          "side fill the GPU; the process's 4 hardware queues hold the encoder, 2 decoders and the "
                          "copies.  --steps a multiple of depth x gang keeps the timed region free of a partly "
                          "filled last round of decodes")
-    ap.add_argument("--gang", type=int, default=16,
+    ap.add_argument("--gang", type=int, default=32,
                     help="batches decoded together by one decoder handle (one raster pass over gang x batch streams: "
                          "a raster step's latency barely grows with its rows)")
     ap.add_argument("--enc-gang", type=int, default=4,

@@ -590,15 +590,17 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
     }
     if (cfg_id) *cfg_id = 1;
-    // Encoder wavefront steps (M = 32 images x up to 48 blocks): many small tiles beat few large ones
-    // (measured encode time per 32-frame batch: 64x32 / 4 waves 149 ms, 32x32 121, 16x32 / 4 waves 114,
-    // 16x32 / 8 waves 112): the per-tile K loop is latency-bound, so the step wants more workgroups.
-    // LBIC_ENC_CFG selects the earlier shapes for A/B runs (results are identical for every shape).
+    // Encoder wavefront steps (n_img images x up to 48 blocks): many small tiles beat few large ones
+    // (measured encode time per 32-frame batch, encoder alone: 64x32 / 4 waves 149 ms, 32x32 121, 16x32 / 4
+    // waves 114, 16x32 / 8 waves 112): the per-tile K loop is latency-bound, so the step wants more
+    // workgroups.  Beside the two ganged decode passes (4 batches per encoder pass) 16x32 / 4 waves (each wave
+    // two K slices) takes 77 us per launch against 122 us for 8 waves: encode phase 100 vs 150 ms per batch.
+    // LBIC_ENC_CFG selects the other shapes for A/B runs (results are identical for every shape).
     switch (g_enc_cfg) {
         case 1: return launch_cfg<64, 32, 4, 2>(g, s);
-        case 2: return launch_cfg<16, 32, 4, 2>(g, s);
+        case 2: return launch_cfg<16, 32, 8, 2>(g, s);
         case 3: return launch_cfg<32, 32, 8, 2>(g, s);
-        default: return launch_cfg<16, 32, 8, 2>(g, s);
+        default: return launch_cfg<16, 32, 4, 2>(g, s);
     }
 }
 

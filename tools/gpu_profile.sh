@@ -2,7 +2,9 @@
 # One GPU session: the PMC passes (FETCH_SIZE, WRITE_SIZE separately) -- the decoder's kernels on a 128x128-frame
 # run whose raster-step shapes equal the 768x768 config's (gang x 32 rows per step), the encoder's GEMMs on
 # 768x768 encode-only passes -- merged into pmc_traffic.json, which the full bench line that follows reads for
-# roofline.traffic; then rocprofv3 kernel-trace stats of the same bench command.  Outputs under gpurun_out/.
+# roofline.traffic; then rocprofv3 kernel-trace stats of the same bench command's timed pipeline (without the
+# serial / two-stage / sub-stream side legs: with them, >1 M traced dispatches, rocprofv3 7.2 crashed once
+# with SIGSEGV in its own thread after the warmup).  Outputs under gpurun_out/.
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -32,6 +34,6 @@ PY
 cp $O/pmc_traffic.json $R/profiles/pmc_traffic.json
 timeout -k 10 400 python3 $R/bench.py > $O/bench.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pk -o run -- \
-    python3 $R/bench.py --cpu-budget 0 --substream-steps 0 > $O/prof_kt.log 2>&1
+    python3 $R/bench.py --cpu-budget 0 --substream-steps 0 --serial-steps 0 > $O/prof_kt.log 2>&1
 cp $(find /tmp/pk -name "*kernel_stats.csv") $O/kernel_stats.csv
 echo done
