@@ -395,24 +395,31 @@ int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, siz
         std::memcpy(w, subs[i].first, 8);
         x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
     }
-    std::vector<uint8_t> cat(total);
-    for (size_t i = 0, off = 0; i < n; off += subs[i].second, ++i) std::memcpy(cat.data() + off, subs[i].first, subs[i].second);
     int rc;
-    if (cat.size() > m->words.bytes && (rc = m->words.alloc(cat.size() + cat.size() / 2 + (1 << 20)))) return rc;
-    // (a page-locked staging buffer here corrupted the stamp slots of the other codec handle's encoder
-    // graph on ROCm 7.2 — a reproducible, unexplained interaction; the pageable copy is kept)
-    HIPCHK(hipMemcpy(m->words.p, cat.data(), cat.size(), hipMemcpyHostToDevice));
+    if (total > m->words.bytes && (rc = m->words.alloc(total + total / 2 + (1 << 20)))) return rc;
+    // each stream straight from the caller's buffer to its word offset: no host-side concatenation (a ganged
+    // pass uploads ~1 GB: allocating, zeroing and filling a host copy of it sat on the decoder's critical
+    // path, and one ~1 GB pageable copy crashed rocprofv3 7.2's kernel trace).  (A page-locked staging buffer
+    // here corrupted the stamp slots of the other codec handle's encoder graph on ROCm 7.2 -- a reproducible,
+    // unexplained interaction; pageable copies are kept.)
+    // stream-ordered on the decoder's stream: the words are rewritten only after that stream's previous
+    // graph (which reads them) has drained, whatever the stream's blocking flags
+    for (size_t i = 0; i < n; ++i)
+        HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(m->words.p) + (size_t)base[i] * 4, subs[i].first, subs[i].second,
+                              hipMemcpyHostToDevice, s));
     // per-stream arrays: sized by the stream count, pointers kept stable for the graphs
     const size_t cap = std::max<size_t>(n, 64);
     if ((rc = m->word_base.alloc(cap * sizeof(long long))) || (rc = m->word_count.alloc(cap * sizeof(int))) ||
         (rc = m->st_x.alloc(cap * sizeof(unsigned long long))) || (rc = m->st_ptr.alloc(cap * sizeof(int))) ||
         (rc = m->st_status.alloc(cap * sizeof(int))))
         return rc;
-    HIPCHK(hipMemcpy(m->word_base.p, base.data(), n * sizeof(long long), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(m->word_count.p, cnt.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(m->st_x.p, x0.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(m->st_ptr.p, ptr.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(m->word_base.p, base.data(), n * sizeof(long long), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(m->word_count.p, cnt.data(), n * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(m->st_x.p, x0.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(m->st_ptr.p, ptr.data(), n * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(m->st_status.p, 0, n * sizeof(int), s));
+    // the host arrays above are locals and the caller's buffers are only borrowed: drain before returning
+    HIPCHK(hipStreamSynchronize(s));
     return LBC_OK;
 }
 
