@@ -119,7 +119,10 @@ int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_
 
 /* decompress() (net:400-452) for a batch of images: streams[i] / lens[i] are the host bitstreams
  * lbc_rans_encode produced.  Strictly raster-serial within an image (the reference format has one
- * rANS stream per image); images are decoded together, rANS decode runs on the GPU. */
+ * rANS stream per image); images are decoded together, rANS decode runs on the GPU.  The streams are
+ * copied to the device in `stream` order (after that stream's earlier work) and the call returns only
+ * once they have been consumed, so the caller may free or reuse its buffers on return; the decode
+ * itself stays asynchronous on `stream`. */
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 
