@@ -1,34 +1,40 @@
 #!/usr/bin/env python3
 """Benchmark: Mpixels/s encode+decode of the block-level masked-conv codec (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), a batch of 32 synthetic
-768x768 frames per GPU.  One step = the reference's timed region of eval_model
-(agents/blkbsdimgcomp_agent.py:591-599) for the whole batch: compress (GPU wavefront closed loop + host
-rANS encode, one stream per image in the reference format) and decompress (GPU raster closed loop with
-GPU rANS decode).  Batches are software-pipelined: the raster decode is a chain of Hb*Wb latency-bound
-steps whose cost barely grows with the rows per step, so each decoder handle decodes `gang` (default 32)
-queued batches in one raster pass, and 2 such passes run side by side (own codec handle + HIP stream each),
-while the next batches are compressed on the GPU (another handle/stream; `enc-gang` (default 4) batches of
-distinct frames per wavefront pass) and entropy coded on host threads.
-The timed region holds exactly `steps` compressions and `steps` decompressions of 32-frame batches, every
-batch fully encoded and fully decoded (bit-exactness of the last one is checked).  The one-decode-in-flight
-pipeline and the non-overlapped serial schedule are reported beside it ("two_stage_schedule",
-"serial_schedule"; --depth 1 --gang 1 / --serial select them).
-Inputs are resident in HBM when the timed region starts.  Weights are the seeded
-synthetic set (lbic.weights, seed = config seed 1337); frames are seeded uint8 noise (no Kodak / no
-checkpoints offline).
+Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), batches of 32 synthetic
+768x768 frames per GPU, in the reference bitstream format (one raster rANS stream per image).  One step =
+the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-599) for one 32-frame batch:
+compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
+rANS decode).  Every decode pass decodes exactly one 32-frame batch (32 frames in flight per pass).
 
-Multi-GPU (torchrun, one process per GPU): every rank codes its own 32 frames (weak scaling); the only
-collectives are a barrier, a MAX of the step time and one all_gather of the per-image rate/distortion
-summary (RCCL over xGMI).
+Schedule of the headline (`value`): a software pipeline over the `--steps` batches.  The encoder (own codec
+handle + HIP stream) compresses batch k+1 while `--depth` decoder handles (own handle + stream each, default
+2) each decode one earlier batch; host rANS runs on a helper thread.  The timed region holds exactly the
+`--steps` compressions and the `--steps` decompressions of the same batches, pipeline fill and drain
+included; inputs are resident in HBM when it starts.  Reported beside it: one decode pass in flight
+(`one_decode_in_flight`), no overlap at all (`serial_schedule`), the gang schedule (`gang_schedule`: one raster
+pass over several queued batches, more frames in flight, not the headline), and the opt-in sub-stream
+format (`substream_format`, not the reference bitstream).
 
-Prints ONE JSON line on rank 0.  See DESIGN.md for the roofline definitions.
+Weights: the seeded synthetic set (lbic.weights) at the config's operating point (`--rate low`: about
+0.13 bpp on these frames, BASELINE.md's B8_lowrate point is 0.117 bpp); `--rate high` is the 12 bpp set.
+Frames: seeded uint8 noise (no Kodak, no checkpoints offline).
+
+Multi-GPU: `--gpus N` relaunches itself under torch.distributed.run (one process per GPU, 127.0.0.1)
+unless WORLD_SIZE is already set.  Images are sharded (every rank codes its own batches: weak scaling);
+the only collectives are barriers, a MAX of the timed region and one all_gather of the per-image
+rate/distortion records (RCCL over xGMI).
+
+Prints ONE JSON line on rank 0.  Roofline, CPU baseline and PMC definitions: DESIGN.md §6.
 """
 import argparse
 import json
-import re
 import math
 import os
+import platform
+import queue
+import re
+import subprocess
 import sys
 import threading
 import time
@@ -38,9 +44,6 @@ PKG = os.path.join(ROOT, "learned-block-based-image-compression_amd")
 for _p in (ROOT, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
-
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 METRIC = "Mpixels/s encode+decode, B8_lowrate N768M96, 768×768; bpp/PSNR vs ref"
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA (dense) peak
@@ -58,68 +61,107 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(arch, sd, H, W, budget_s):
-    """The oracle (numpy fp32 + C rANS, one thread) on a bounded sample: the first R block rows of one
-    frame, encode + decode; R chosen so the sample takes about `budget_s`."""
-    from threadpoolctl import threadpool_limits
-    from oracle import oracle as O
-    img = np.random.default_rng(0).integers(0, 256, (3, H, W), dtype=np.uint8).astype(np.float32) / 255.0 - 0.5
-    xb = O.image_to_blocks(img, arch.B)
-    Hb, Wb = xb.shape[:2]
-    with threadpool_limits(limits=1):
-        codec = O.OracleCodec(arch, sd)
-
-        def run(rows):
-            t0 = time.perf_counter()
-            out = codec.compress(xb, rows=rows)
-            codec.decompress(out["bytes"], Hb, Wb, rows=rows)
-            return time.perf_counter() - t0
-
-        t1 = run(1)
-        rows = int(max(1, min(Hb, math.floor(budget_s / max(t1, 1e-3)))))
-        t = run(rows) if rows > 1 else t1
-    px = rows * arch.B * W
-    return dict(value=px / t / 1e6, unit="Mpixels/s", cores=1, kind="port",
-                sample=f"oracle/oracle.py (numpy fp32, 1 thread, C rANS) encode+decode of the first {rows} of {Hb} "
-                       f"block rows of one {H}x{W} frame ({rows * Wb} blocks, {t:.1f} s); per-block cost is "
-                       f"content-independent, so the full frame extrapolates to {t * Hb / rows:.0f} s")
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
+    ap.add_argument("--steps", type=int, default=20, help="timed batches (each encoded and decoded in the region)")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed pipeline batches before the timed region")
+    ap.add_argument("--batch", type=int, default=32, help="frames per batch (per GPU)")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
     ap.add_argument("--height", type=int, default=0, help="frame height (default: --size)")
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
-    ap.add_argument("--sample-every", type=int, default=32, help="kernel-event sampling period (steps)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
-    ap.add_argument("--serial", action="store_true", help="no encode/decode overlap between consecutive batches")
-    ap.add_argument("--depth", type=int, default=0,
-                    help="decoder handles in flight beside the encoder (1 = two-stage pipeline; default 2).  The "
-                         "raster decode is a latency-bound chain: more rows per step (--gang) and two chains side by "
-                         "side fill the GPU; the process's 4 hardware queues hold the encoder, 2 decoders and the "
-                         "copies.  --steps a multiple of depth x gang keeps the timed region free of a partly "
-                         "filled last round of decodes")
-    ap.add_argument("--gang", type=int, default=32,
-                    help="batches decoded together by one decoder handle (one raster pass over gang x batch streams: "
-                         "a raster step's latency barely grows with its rows)")
-    ap.add_argument("--enc-gang", type=int, default=4,
-                    help="batches compressed together in one wavefront pass (steps must be a multiple)")
-    ap.add_argument("--enc-lds-floor", type=int, default=int(os.environ.get("LBIC_ENC_LDS_FLOOR", "0")),
-                    help="LDS bytes reserved per encoder GEMM workgroup in the pipeline (>80 KB: one per CU)")
-    ap.add_argument("--encode-only", type=int, default=0,
-                    help="profiling aid: run this many encoder passes (enc-gang batches each) and exit (no JSON line)")
-    ap.add_argument("--serial-steps", type=int, default=1, help="extra non-overlapped steps reported apart (0 = skip)")
-    ap.add_argument("--substream-steps", type=int, default=2,
-                    help="extra steps in the opt-in per-row sub-stream format, reported apart (0 = skip)")
-    args = ap.parse_args()
+    ap.add_argument("--rate", default="low", choices=("low", "high"), help="synthetic weight operating point")
+    ap.add_argument("--depth", type=int, default=2, help="decode passes in flight beside the encoder (0 = serial)")
+    ap.add_argument("--sample-every", type=int, default=16, help="kernel timing-stamp sampling period (steps)")
+    ap.add_argument("--cpu-budget", type=float, default=24.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--side-steps", type=int, default=2,
+                    help="batches of the one-decode-in-flight and serial schedules reported beside (0 = skip)")
+    ap.add_argument("--gang", type=int, default=8, help="batches per raster pass of the gang schedule (0 = skip)")
+    ap.add_argument("--substream-steps", type=int, default=2, help="batches in the sub-stream format (0 = skip)")
+    ap.add_argument("--encode-only", type=int, default=0, help="profiling aid: this many encoder passes, no JSON")
+    return ap.parse_args(argv)
+
+
+def relaunch_distributed(args):
+    """--gpus N > 1 without a torch.distributed environment: run this script under torch.distributed.run
+    (one process per GPU) as a child process -- nothing here has touched the GPU -- and exit with its code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("[bench] relaunch:", " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(arch, sd, H, W, budget_s):
+    """oracle/torch_ref.py (torch-CPU restatement of the reference's compress/decompress, parity-checked
+    against the reference's golden vectors) on the host cores: encode+decode of the first R block rows of one
+    frame (per-block cost is content-independent), at 1 thread (eval_model's setting,
+    agents/blkbsdimgcomp_agent.py:565-566) and at every thread the box grants."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    from oracle.torch_ref import TorchRef
+    img = np.random.default_rng(0).integers(0, 256, (3, H, W), dtype=np.uint8).astype(np.float32) / 255.0 - 0.5
+    xb = O.image_to_blocks(img, arch.B)
+    Hb, Wb = xb.shape[:2]
+    ref = TorchRef(arch, sd)
+    model, nproc = cpu_info()
+    threads_all = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+    prev = torch.get_num_threads()
+    res = {}
+    for th in sorted({1, threads_all}):
+        torch.set_num_threads(th)
+
+        def run(rows):
+            t0 = time.perf_counter()
+            out = ref.compress(xb, rows=rows)
+            ref.decompress(out["bytes"], Hb, Wb, rows=rows)
+            return time.perf_counter() - t0
+
+        t1 = run(1)
+        rows = int(max(1, min(Hb, math.floor(budget_s / 2 / max(t1, 1e-3)))))
+        t = run(rows) if rows > 1 else t1
+        res[th] = (rows * arch.B * W / t / 1e6, rows, t)
+    torch.set_num_threads(prev)
+    v_all, rows_all, t_all = res[threads_all]
+    v1, rows1, t1_ = res[1]
+    return dict(value=round(v_all, 6), unit="Mpixels/s", cores=threads_all, kind="port",
+                sample=f"oracle/torch_ref.py (torch-CPU fp32 restatement of compress/decompress, C rANS) encode+decode "
+                       f"of the first {rows_all} of {Hb} block rows of one {H}x{W} frame at {threads_all} threads "
+                       f"({t_all:.1f} s); per-block cost is content-independent",
+                single_thread=dict(value=round(v1, 6), cores=1, rows=rows1, seconds=round(t1_, 2)),
+                cpu_model=model, nproc=nproc)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args))
+
+    import numpy as np
+    import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     dist = world > 1
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -129,9 +171,9 @@ def main():
 
     import types
     from lbic.arch import Arch
+    from lbic.layout import image_to_blocks
     from lbic.model import BlockBasedImgCompLossyNetv9
     from lbic.weights import synth_state_dict
-    from lbic.layout import image_to_blocks
 
     B, KS, N, M = CONFIGS[args.config]
     arch = Arch(B, KS, N, M)
@@ -139,7 +181,8 @@ def main():
     H = args.height or args.size
     Hb, Wb = H // B, W // B
     cfg = types.SimpleNamespace(block_size=B, KS=list(KS), N=N, M=M, gpu_device=local)
-    sd = synth_state_dict(arch, 1337)
+    sd = synth_state_dict(arch, 1337, rate=args.rate)
+    n = args.batch
 
     def make_model():
         m = BlockBasedImgCompLossyNetv9(cfg, device=dev)
@@ -147,30 +190,27 @@ def main():
         m.update(force=True)
         return m
 
-    # codec handles with their own workspaces and reconstruction buffers: one encoder side and `depth`
-    # decoder sides of the pipeline, each on its own HIP stream (created back to back so they land on
-    # distinct hardware queues)
-    depth = 0 if args.serial else (args.depth or 2)
+    depth = max(args.depth, 0)
+    ndec = max(depth, 2 if args.gang else 1, 1)
     enc_model = make_model()
-    dec_models = [make_model() for _ in range(max(depth, 1))]
-    if depth and args.enc_lds_floor:
-        enc_model.set_encoder_lds_floor(args.enc_lds_floor)
+    dec_models = [make_model() for _ in range(ndec)]
     s_enc = torch.cuda.Stream(dev)
     s_decs = [torch.cuda.Stream(dev) for _ in dec_models]
     handles = [enc_model] + dec_models
     plock = threading.Lock()
 
-    n = args.batch
-    # an encoder pass over `egang` batches compresses egang x n distinct frames (batch e = frames e*n .. e*n+n-1)
-    egang = max(1, args.enc_gang) if depth else 1
-    if args.steps % egang:
-        raise SystemExit("--steps must be a multiple of --enc-gang")
-    frames = np.stack([image_to_blocks(np.random.default_rng(rank * n * egang + k).integers(0, 256, (3, H, W),
-                                                                                       dtype=np.uint8)
-                                       .astype(np.float32) / 255.0 - 0.5, B) for k in range(n * egang)])
+    # two distinct 32-frame sets per rank (batch k codes set k % 2); the gang schedule's encoder passes
+    # compress `gang` batches of distinct frames at once
+    nsets = max(2, args.gang)
+    frames = np.stack([image_to_blocks(np.random.default_rng(rank * n * nsets + k).integers(0, 256, (3, H, W),
+                                                                                    dtype=np.uint8)
+                                       .astype(np.float32) / 255.0 - 0.5, B) for k in range(n * nsets)])
     xb_all = torch.from_numpy(frames).to(dev)
-    xb = xb_all[:n]
     del frames
+
+    def frames_of(k):
+        s = k % 2
+        return xb_all[s * n:(s + 1) * n]
 
     def barrier():
         if dist:
@@ -184,14 +224,11 @@ def main():
             v = float(t.item())
         return v
 
-    def compress_side(ph, egang=1):
-        """compress (GPU) on the encoder stream: one batch, or `egang` batches in one wavefront pass -> a list of
-        per-batch results"""
+    def compress_side(ph, xb):
+        """GPU compress on the encoder stream; symbols/indexes DMA'd into page-locked host buffers there."""
         t0 = time.perf_counter()
         with torch.cuda.stream(s_enc):
-            r = enc_model.compress_batch(xb if egang == 1 else xb_all)
-            # symbols/indexes for the host rANS: DMA into page-locked buffers (torch's caching host allocator)
-            # on the encoder's stream, ahead of the next batch's compress
+            r = enc_model.compress_batch(xb)
             for k in ("symbols", "indexes"):
                 h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
                 h.copy_(r[k], non_blocking=True)
@@ -199,20 +236,14 @@ def main():
             s_enc.synchronize()
         with plock:
             ph["encode"] += time.perf_counter() - t0
-        return [dict({k: (v[e * n:(e + 1) * n] if v is not None else None) for k, v in r.items()}, frames=e)
-                for e in range(egang)]
+        return r
 
     def entropy_side(r, fmt, ph):
-        """host rANS of a compressed batch (reference format: one stream per image) -> streams"""
         t0 = time.perf_counter()
-        st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)   # host tensors
+        st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
         with plock:
             ph["entropy"] += time.perf_counter() - t0
         return st
-
-    def encode_side(fmt, ph):
-        r = compress_side(ph)[0]
-        return r, entropy_side(r, fmt, ph)
 
     def decode_side(i, st, fmt, ph):
         t0 = time.perf_counter()
@@ -225,170 +256,160 @@ def main():
 
     def collect_stats():
         ks = {}
-        for m_ in handles:           # merge the handles' per-kernel records
+        for m_ in handles:
             for name, st_ in (m_.profile_end() or {}).items():
-                acc = ks.setdefault(name, dict(launches=0, total_launches=0, total_ms=0.0, flops=0.0, bytes=0.0))
-                for k_ in acc:
+                acc = ks.setdefault(name, {k: 0.0 for k in st_})
+                for k_ in st_:
                     acc[k_] += st_[k_]
         return ks
 
-    def run(fmt, steps, warmup, depth, label, prof=False, gang=1, egang=1):
-        """`steps` timed batches.  depth 0: encode, entropy, decode one after another.  depth D >= 1: a software
-        pipeline -- D decoder handles (own streams, helper threads; ctypes drops the GIL) decode `gang` batches
-        per raster pass from a queue of at most D*gang encoded batches, while this thread compresses the next
-        batches on the GPU and a helper thread entropy codes them on the host.  The timed region holds exactly
-        `steps` encodes and `steps` decodes: the pipeline is primed with D*gang encodes and drained with D*gang
-        decodes outside it (its steady state)."""
+    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0):
+        """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
+        (or `gang` batches in one wavefront pass) while a helper thread entropy codes the previous one and
+        `depth` decoder threads each decode `gang` queued batches per raster pass (their own handles and
+        streams; ctypes drops the GIL).  depth 0: encode, entropy, decode one after another.
+        Returns (seconds, phase seconds, last decoded (record, streams, zhat), kernel stats)."""
         ph = dict(encode=0.0, entropy=0.0, decode=0.0)
-        scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
-        for i in range(warmup):
-            for d in range(len(dec_models)):          # every decoder handle builds its graphs
-                r, st = encode_side(fmt, scratch)
-                decode_side(d, list(st) * gang, fmt, scratch)
-            if egang > 1:                             # and the encoder its ganged graph
-                compress_side(scratch, egang)
-            log(f"[rank {rank}] {label} warmup {i + 1}/{warmup} done")
-        def prof_begin():   # launch counts cover the timed region only (same sampling period: graphs are kept)
-            if prof:
-                for m_ in handles:
-                    m_.profile_begin(args.sample_every)
-        last = []
-        if depth == 0:
-            prof_begin()
-            barrier()
-            t0 = time.perf_counter()
-            for i in range(steps):
-                r, st = encode_side(fmt, ph)
-                last = [(r, st, decode_side(0, st, fmt, ph))]
-                log(f"[rank {rank}] {label} step {i + 1}/{steps}: {time.perf_counter() - t0:.2f} s")
-            barrier()
-            dt = max_over_ranks(time.perf_counter() - t0)
-            return dt, ph, (last[-1] if last else None), collect_stats() if prof else None
-        import queue
-        primed = []                                 # prime (with the encoder's own pass shape: graphs are kept)
-        while len(primed) < depth * gang:
-            primed += [(r_, entropy_side(r_, fmt, scratch)) for r_ in compress_side(scratch, egang)]
-        del primed[depth * gang:]
-        prof_begin()
-        q = queue.Queue(maxsize=depth * gang)      # encoded batches waiting for a decoder
-        eq = queue.Queue(maxsize=1)                # compressed batches waiting for the host rANS
-        done, pending = [], []
-        glock = threading.Lock()
-
-        def decoder(i):
-            while True:
-                items, end = [], False
-                with glock:                       # one decoder gathers its whole gang
-                    while len(items) < gang:      # gang decode: up to `gang` queued batches in one raster pass
-                        item = q.get()
-                        if item is None:
-                            end = True
-                            break
-                        items.append(item)
-                if items:
-                    z_ = decode_side(i, [b for _, (_, st_) in items for b in st_], fmt, ph)
-                    with plock:
-                        for k, (j, (r_, st_)) in enumerate(items):
-                            done.append((j, r_, st_, z_[k * n:(k + 1) * n]))
-                    log(f"[rank {rank}] {label} batches {[j for j, _ in items]} decoded (decoder {i}): "
-                        f"{time.perf_counter() - t0:.2f} s")
-                if end:
-                    q.put(None)                   # pass the end mark on to the other decoders
-                    return
-
-        def entropy_worker():
-            # host rANS of batch k beside the GPU compress of batch k+1 (this thread's pool drops the GIL);
-            # batches past `steps` are entropy coded inside the timed region but decoded after it (the drain)
-            while True:
-                item = eq.get()
-                if item is None:
-                    q.put(None)
-                    return
-                j0, rs_ = item
-                for e, r_ in enumerate(rs_):
-                    st_ = entropy_side(r_, fmt, ph)
-                    if j0 + e < steps:
-                        q.put((j0 + e, (r_, st_)))
-                    else:
-                        pending.append((r_, st_))
-
-        ths = [threading.Thread(target=decoder, args=(i,)) for i in range(depth)]
-        eth = threading.Thread(target=entropy_worker)
+        if prof:
+            for m_ in handles:
+                m_.profile_begin(args.sample_every)
         barrier()
         t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for k, e in enumerate(primed[:steps]):
-            q.put((k, e))
-        pending.extend(primed[steps:])
-        eth.start()
-        for i in range(0, steps, egang):
-            eq.put((len(primed) + i, compress_side(ph, egang)))
-        eq.put(None)
-        eth.join()
-        for th in ths:
-            th.join()
+        done = dict(count=0, last=None)      # only the latest batch is kept (its pinned / device buffers)
+
+        def finish(k_, r_, st_, z_):
+            with plock:
+                done["count"] += 1
+                if done["last"] is None or k_ > done["last"][0]:
+                    done["last"] = (k_, r_, st_, z_)
+        if depth == 0:
+            for k in range(steps):
+                r = compress_side(ph, frames_of(base + k))
+                st = entropy_side(r, fmt, ph)
+                finish(base + k, r, st, decode_side(0, st, fmt, ph))
+        else:
+            q = queue.Queue(maxsize=depth * gang)      # encoded batches waiting for a decoder
+            eq = queue.Queue(maxsize=1)                # compressed batches waiting for the host rANS
+            glock = threading.Lock()
+
+            def decoder(i):
+                while True:
+                    items, end = [], False
+                    with glock:                        # one decoder gathers its whole gang
+                        while len(items) < gang:
+                            it = q.get()
+                            if it is None:
+                                end = True
+                                break
+                            items.append(it)
+                    if items:
+                        z_ = decode_side(i, [b for (_, _, st_) in items for b in st_], fmt, ph)
+                        for j, (k_, r_, st_) in enumerate(items):
+                            finish(k_, r_, st_, z_[j * n:(j + 1) * n])
+                    if end:
+                        q.put(None)
+                        return
+
+            def entropy_worker():
+                while True:
+                    it = eq.get()
+                    if it is None:
+                        q.put(None)
+                        return
+                    for k_, r_ in it:
+                        q.put((k_, r_, entropy_side(r_, fmt, ph)))
+
+            ths = [threading.Thread(target=decoder, args=(i,)) for i in range(depth)]
+            eth = threading.Thread(target=entropy_worker)
+            for th in ths + [eth]:
+                th.start()
+            for k in range(0, steps, gang):
+                g = min(gang, steps - k)
+                if g == 1:
+                    eq.put([(base + k, compress_side(ph, frames_of(base + k)))])
+                else:       # one wavefront pass over g batches of distinct frames
+                    r = compress_side(ph, xb_all[:g * n])
+                    eq.put([(base + k + e, {kk: (v[e * n:(e + 1) * n] if v is not None else None)
+                                            for kk, v in r.items()}) for e in range(g)])
+            eq.put(None)
+            eth.join()
+            for th in ths:
+                th.join()
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         ks = collect_stats() if prof else None
-        for k in range(0, len(pending), gang):                         # drain (outside the timed region)
-            decode_side((k // gang) % depth, [b for _, st_ in pending[k:k + gang] for b in st_], fmt, scratch)
-        j, r_, st_, z_ = max(done, key=lambda e: e[0])
-        return dt, ph, (r_, st_, z_), ks
+        if label:
+            log(f"[rank {rank}] {label}: {steps} batches in {dt:.2f} s")
+        if done["count"] != steps:
+            raise RuntimeError(f"{label}: {done['count']} of {steps} batches decoded")
+        return dt, ph, done["last"][1:], ks
 
-    # sampling is part of the captured graphs: enable it before the warmup builds them
+    def summary(dt, ph, k, **extra):
+        return dict(value=round(world * n * H * W / (dt / k) / 1e6, 4), ms_per_step=round(dt / k * 1e3, 2),
+                    steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in ph.items()}, **extra)
+
+    # sampling is part of the captured graphs: enable it before the first capture
     for m_ in handles:
         m_.profile_begin(args.sample_every)
-    gang = max(1, args.gang) if depth else 1
-    if args.encode_only:      # e.g. rocprofv3 --pmc on the encoder's real launch shapes (tools/gpu_profile.sh)
+    if args.encode_only:      # e.g. rocprofv3 --pmc on the encoder's launch shapes
         for i in range(args.encode_only):
-            compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), egang)
-            log(f"[rank {rank}] encoder pass {i + 1}/{args.encode_only} ({egang} batches) done")
+            compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), frames_of(i))
+            log(f"[rank {rank}] encoder pass {i + 1}/{args.encode_only} done")
         return
-    run("reference", 0, args.warmup, 0, "warmup", gang=gang, egang=egang)
-    dt, phase, (r, streams, z), kstats = run("reference", args.steps, 0, depth, "reference", prof=True, gang=gang,
-                                             egang=egang)
 
-    def summary(dts, phs, k):
-        return dict(value=round(world * n * H * W / (dts / k) / 1e6, 4), ms_per_step=round(dts / k * 1e3, 2),
-                    steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in phs.items()})
-    serial = two_stage = None
-    if depth and args.serial_steps > 0:     # the same batches without the overlap, for reference
-        dts, phs, _, _ = run("reference", args.serial_steps, 1 if gang * egang > 1 else 0, 0, "serial")
-        serial = summary(dts, phs, args.serial_steps)
-    if depth > 1 and args.serial_steps > 0:  # one decoder in flight
-        dts, phs, _, _ = run("reference", 2 * args.serial_steps, 1 if gang * egang > 1 else 0, 1, "two-stage")
-        two_stage = summary(dts, phs, 2 * args.serial_steps)
+    # warmup: every decoder handle builds its row graphs, then `warmup` batches through the pipeline
+    scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
+    r0 = compress_side(scratch, frames_of(0))
+    st0 = entropy_side(r0, "reference", scratch)
+    for i in range(len(dec_models)):
+        decode_side(i, st0, "reference", scratch)
+    if args.warmup > 0:
+        pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup")
 
-    # --- opt-in sub-stream format (SURVEY H1b): same encoder, one rANS stream per block row, wavefront
-    #     decode.  Reported apart from the headline (which stays on the reference bitstream format).
+    # ---- headline: the reference bitstream format, one 32-frame batch per decode pass
+    dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline")
+
+    side = {}
+    if args.side_steps > 0 and depth != 1:
+        d_, p_, _, _ = pipeline(args.side_steps, 1, label="one decode in flight")
+        side["one_decode_in_flight"] = summary(d_, p_, args.side_steps, frames_in_flight_per_decode_pass=n,
+                                               decode_passes_in_flight=1)
+    if args.side_steps > 0 and depth != 0:
+        d_, p_, _, _ = pipeline(args.side_steps, 0, label="serial")
+        side["serial_schedule"] = summary(d_, p_, args.side_steps)
+    gang_s = None
+    if args.gang > 1 and depth >= 1:
+        gsteps = 2 * args.gang                    # one gang pass per decoder handle, both in the region
+        # (the decoders' graphs for gang x n streams are built by an untimed pass first)
+        pipeline(2 * args.gang, 2, gang=args.gang, label="gang warmup")
+        d_, p_, _, _ = pipeline(gsteps, 2, gang=args.gang, label="gang")
+        gang_s = summary(d_, p_, gsteps, frames_in_flight_per_decode_pass=args.gang * n, decode_passes_in_flight=2,
+                         batches_per_encode_pass=args.gang,
+                         note="not the headline: a raster pass over several queued batches (more frames in flight "
+                              "than the batch-32 config)")
     sub = None
     if args.substream_steps > 0:
-        run("rows", 0, 1, 0, "rows warmup")
-        dts, phs, (rs, ss, zs), _ = run("rows", args.substream_steps, 0, depth, "rows")
-        sub = dict(value=round(world * n * H * W / (dts / args.substream_steps) / 1e6, 4),
-                   ms_per_step=round(dts / args.substream_steps * 1e3, 2), steps=args.substream_steps,
-                   bpp=round(float(np.mean([len(b) * 8.0 / (H * W) for b in ss])), 5),
-                   enc_dec_bit_exact_rank0=bool(torch.equal(zs, rs["zhat"])),
-                   phases_ms_per_step={k: round(v / args.substream_steps * 1e3, 2) for k, v in phs.items()})
+        pipeline(max(depth, 1), max(depth, 1), fmt="rows", label="rows warmup")
+        d_, p_, (rs, ss, zs), _ = pipeline(args.substream_steps, max(depth, 1), fmt="rows", label="rows")
+        sub = summary(d_, p_, args.substream_steps,
+                      bpp=round(float(np.mean([len(b) * 8.0 / (H * W) for b in ss])), 5),
+                      enc_dec_bit_exact=bool(torch.equal(zs, rs["zhat"])),
+                      note="opt-in per-block-row sub-stream container (not the reference bitstream)")
 
-    # --- quality / consistency of the last decoded batch (outside the timed region)
+    # ---- quality of the last decoded batch (outside the timed region) + parity against the reference's
+    #      full-frame fixture (tests/golden), when this is its configuration
     bit_exact = bool(torch.equal(z, r["zhat"]))
-    xq = xb_all[r["frames"] * n:(r["frames"] + 1) * n]      # the frames of that batch
+    xq = frames_of(max(0, args.steps - 1))
     sse = ((z - xq) ** 2).double().sum(dim=(1, 2, 3))
     rec = torch.stack([torch.tensor([float(len(s)) for s in streams], dtype=torch.float64, device=dev), sse,
                        torch.full((n,), float(H * W * 3), dtype=torch.float64, device=dev)], dim=1)
-    if dist:
-        allrec = [torch.empty_like(rec) for _ in range(world)]
-        torch.distributed.all_gather(allrec, rec)
-        rec = torch.cat(allrec)
-        ok = torch.tensor([1.0 if bit_exact else 0.0], device=dev)
-        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
-        bit_exact = bool(ok.item() == 1.0)
+    rec, bit_exact = gather_records(rec, bit_exact, dist)
     rec = rec.cpu().numpy()
     bpp = float(np.mean(rec[:, 0] * 8.0 / (H * W)))
-    mse = rec[:, 1] / rec[:, 2]
-    psnr = float(np.mean(-10 * np.log10(mse)))
+    psnr = float(np.mean(-10 * np.log10(rec[:, 1] / rec[:, 2])))
+    vs_ref = None
+    if rank == 0:
+        vs_ref = compare_full_frame_fixture(enc_model, args, arch, dev)
 
     if rank != 0:
         if dist:
@@ -396,46 +417,9 @@ def main():
         return
 
     ms_step = dt / args.steps * 1e3
-    px_total = world * n * H * W
-    value = px_total / (dt / args.steps) / 1e6
+    value = world * n * H * W / (dt / args.steps) / 1e6
 
-    # --- roofline of the dominant kernel: launch spans of the sampled launches (in-kernel stamps on the
-    #     GPU's 100 MHz clock, last replay of each graph in the timed region)
-    roof = None
-    kernels = {}
-    if kstats:
-        for name, s in kstats.items():
-            avg = s["total_ms"] / max(s["launches"], 1)
-            kernels[name] = dict(launches_sampled=s["launches"], launches_total=s["total_launches"],
-                                 avg_us=round(avg * 1e3, 3),
-                                 est_share_of_step=round(avg * s["total_launches"] / 1e3 / dt, 4))
-        # dominant kernel: sampled average duration x true launch count over the timed region
-        dom = max(kstats, key=lambda k: kstats[k]["total_ms"] / max(kstats[k]["launches"], 1) * kstats[k]["total_launches"])
-        s = kstats[dom]
-        t_s = s["total_ms"] / 1e3
-        ai = s["flops"] / s["bytes"] if s["bytes"] else float("inf")
-        ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
-        if s["flops"] > 0 and ai >= ridge:
-            ach, peak, unit, bound = s["flops"] / t_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
-        else:
-            ach, peak, unit, bound = s["bytes"] / t_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
-        traffic = None
-        tfile = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/pmc_summary.py), HBM bytes per launch
-            with open(tfile) as fh:
-                pm = json.load(fh)
-            fam = re.sub(r"<.*>$", "", dom)
-            if fam in pm and "hbm_bytes_per_dispatch" in pm[fam]:
-                traffic = round(pm[fam]["hbm_bytes_per_dispatch"])
-        roof = dict(kernel=dom, bound=bound, achieved=round(ach, 3), peak=peak, unit=unit,
-                    frac=round(ach / peak, 5), traffic=traffic,
-                    avg_launch_us=round(s["total_ms"] / s["launches"] * 1e3, 3),
-                    algorithmic_per_launch=dict(flops=s["flops"] / s["launches"], bytes=s["bytes"] / s["launches"]),
-                    arithmetic_intensity=round(ai, 2))
-        mfma_frac = sum(v["flops"] for v in kstats.values()) / (sum(v["total_ms"] for v in kstats.values()) / 1e3) \
-            / (PEAK_FP32_TFLOPS * 1e12)
-        roof["all_kernels_mfma_frac"] = round(mfma_frac, 5)
-    # whole-step algorithmic work
+    roof, kernels = roofline(kstats, dt)
     mac_enc, mac_dec = arch.live_macs_per_block()
     step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
     cpu = None
@@ -446,31 +430,121 @@ def main():
         "metric": METRIC, "value": round(value, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: seeded uint8 noise frames, seeded synthetic weights (no checkpoints / Kodak offline)",
-        "config": {"workload": f"{args.config} N{N}M{M}, batch of {n} synthetic {H}x{W} frames per GPU, "
-                               "encode+decode in the reference bitstream format (one raster rANS stream per image)",
+        "data": f"synthetic: seeded uint8 noise frames, seeded synthetic weights at the '{args.rate}' operating point "
+                "(no checkpoints / Kodak offline)",
+        "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
+                               f"in the reference bitstream format (one raster rANS stream per image); each decode pass "
+                               f"decodes one {n}-frame batch ({n} frames in flight per pass), {depth} pass(es) in flight "
+                               "beside the encoder",
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
-                   "global_batch": n * world,
+                   "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
+                   "decode_passes_in_flight": depth, "frames_per_encode_pass": n,
                    "schedule": "serial: encode, entropy, decode per batch" if depth == 0 else
-                   f"software pipeline: {depth} raster decode pass(es) in flight (one codec handle + HIP stream "
-                   f"each), each over {gang} queued batches, beside the GPU compress and host rANS of the next "
-                   f"batches (own handle + stream, host threads); each timed step = one full encode and one full "
-                   f"decode of a {n}-frame batch",
-                   "decode_passes_in_flight": depth, "batches_per_decode_pass": gang,
-                   "batches_per_encode_pass": egang},
+                   f"pipeline: encoder (own handle + stream) compresses batch k+1 while {depth} decoder handle(s) "
+                   "(own handle + stream each) decode earlier batches, host rANS on a helper thread; the timed "
+                   "region holds the compress and decompress of the same batches, fill and drain included"},
         "roofline": roof, "cpu_baseline": cpu,
-        "quality": {"bpp": round(bpp, 5), "psnr_db": round(psnr, 3), "enc_dec_bit_exact": bit_exact},
+        "quality": {"rate_point": args.rate, "bpp": round(bpp, 5), "psnr_db": round(psnr, 3),
+                    "enc_dec_bit_exact": bit_exact, "vs_ref": vs_ref},
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
         "step_algorithmic_tflop": round(step_flops / 1e12, 3),
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
         "kernels": kernels,
-        "serial_schedule": serial,
-        "two_stage_schedule": two_stage,
+        **side,
+        "gang_schedule": gang_s,
         "substream_format": sub,
     }
     print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def gather_records(rec, ok, dist):
+    """The run's only data collective: every rank's per-image [bytes, SSE, n_px] records all-gathered (RCCL over
+    xGMI on the GPU box, gloo in the CPU test) and the encoder/decoder agreement MIN-reduced."""
+    import torch
+    if not dist:
+        return rec, ok
+    import torch.distributed as tdist
+    allrec = [torch.empty_like(rec) for _ in range(tdist.get_world_size())]
+    tdist.all_gather(allrec, rec)
+    flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=rec.device)
+    tdist.all_reduce(flag, op=tdist.ReduceOp.MIN)
+    return torch.cat(allrec), bool(flag.item() == 1.0)
+
+
+def roofline(kstats, dt):
+    """Dominant kernel family (sampled mean launch period x true launch count over the timed region) against
+    its roofline.  Durations are the in-kernel timing stamps of the sampled launches executed in the timed
+    region (lbc_profile_*): `avg_launch_us` is the launch-to-launch period in the stream chain (end of the
+    previous launch -> end of this one: the launch's span plus the boundary in front of it, which is what a
+    dispatch-to-completion trace measures), `avg_span_us` the workgroups' own span."""
+    if not kstats:
+        return None, {}
+    kernels = {}
+    for name, s in kstats.items():
+        span = s["total_ms"] / max(s["launches"], 1)
+        per = s["total_ms_chain"] / s["launches_chain"] if s["launches_chain"] else span
+        kernels[name] = dict(launches_sampled=int(s["launches"]), launches_total=int(s["total_launches"]),
+                             avg_span_us=round(span * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
+                             est_share_of_step=round(per * s["total_launches"] / 1e3 / dt, 4))
+    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_total"])
+    s = kstats[dom]
+    per_launch_s = kernels[dom]["avg_launch_us"] * 1e-6
+    fl, by = s["flops"] / s["launches"], s["bytes"] / s["launches"]
+    ai = fl / by if by else float("inf")
+    ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    if fl > 0 and ai >= ridge:
+        ach, peak, unit, bound = fl / per_launch_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
+    else:
+        ach, peak, unit, bound = by / per_launch_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):       # rocprofv3 PMC passes of this command (tools/gpu_profile.sh)
+        with open(tfile) as fh:
+            pm = json.load(fh)
+        fam = re.sub(r"<.*>$", "", dom)
+        if fam in pm and "hbm_bytes_per_dispatch" in pm[fam]:
+            traffic = round(pm[fam]["hbm_bytes_per_dispatch"])
+    roof = dict(kernel=dom, bound=bound, achieved=round(ach, 4), peak=peak, unit=unit, frac=round(ach / peak, 5),
+                traffic=traffic, avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],
+                algorithmic_per_launch=dict(flops=round(fl), bytes=round(by)), arithmetic_intensity=round(ai, 2),
+                frac_of_span=round((fl / (kernels[dom]["avg_span_us"] * 1e-6) / 1e12 / peak) if bound == "mfma" else
+                                   (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5))
+    return roof, kernels
+
+
+def compare_full_frame_fixture(model, args, arch, dev):
+    """The reference's own full-frame closed loop (tests/golden/frame_b8_lowrate.npz, generated from
+    graphs/models/BlockBasedImgCompLossy_net.py:319-361 by tests/golden/gen_golden.py) against this
+    library on the same frame and weights: symbol / index mismatches, zhat difference, PSNR and
+    estimated-bpp deltas.  None when the configuration differs or the fixture is absent."""
+    import numpy as np
+    import torch
+    path = os.path.join(ROOT, "tests", "golden", "frame_b8_lowrate.npz")
+    if not os.path.exists(path) or args.config != "B8_lowrate":
+        return None
+    g = dict(np.load(path))
+    if str(g["rate"]) != args.rate:
+        return None
+    x = torch.from_numpy(g["x"])[None].to(dev)
+    r = model.compress_batch(x, want_bits=True)
+    torch.cuda.synchronize(dev)
+    sym = r["symbols"][0].cpu().numpy()
+    idx = r["indexes"][0].cpu().numpy()
+    zh = r["zhat"][0].cpu().numpy()
+    bits = r["bits"][0].cpu().numpy()
+    H, W = g["image"].shape[1:]
+    x0 = g["x"].astype(np.float64)
+
+    def psnr(z):
+        return float(-10 * np.log10(np.mean((z.astype(np.float64) - x0) ** 2)))
+    zref = g["zhat"]
+    return dict(fixture="tests/golden/frame_b8_lowrate.npz (reference closed loop, one 768x768 frame)",
+                symbol_mismatches=int((sym != g["symbols"]).sum()), index_mismatches=int((idx != g["indexes"]).sum()),
+                symbols=int(sym.size), zhat_max_abs_diff=float(np.abs(zh - zref).max()),
+                psnr_db=round(psnr(zh), 5), psnr_ref_db=round(psnr(zref), 5),
+                est_bpp=round(float(bits.sum()) / (H * W), 6), est_bpp_ref=round(float(g["bits"].sum()) / (H * W), 6))
 
 
 if __name__ == "__main__":

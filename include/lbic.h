@@ -120,9 +120,9 @@ int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_
 /* decompress() (net:400-452) for a batch of images: streams[i] / lens[i] are the host bitstreams
  * lbc_rans_encode produced.  Strictly raster-serial within an image (the reference format has one
  * rANS stream per image); images are decoded together, rANS decode runs on the GPU.  The streams are
- * copied to the device in `stream` order (after that stream's earlier work) and the call returns only
- * once they have been consumed, so the caller may free or reuse its buffers on return; the decode
- * itself stays asynchronous on `stream`. */
+ * copied to the device in `stream` order (after that stream's earlier work).  The call is synchronous:
+ * it returns after the whole decode has finished on `stream` (it reads back the per-stream status to
+ * report a corrupt bitstream), so the caller may free or reuse its buffers on return. */
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 
@@ -142,17 +142,22 @@ const char *lbc_last_error(void);
  * total milliseconds of the encode and decode phases. */
 int lbc_last_timing(const lbc_model *m, double *enc_ms, double *dec_ms);
 
-/* Per-kernel HIP-event instrumentation (bench.py's roofline): while enabled, every `sample_every`-th
- * wavefront / raster step brackets each kernel launch with a pair of events on the launch stream and
- * records the launch's algorithmic FLOPs and bytes.  lbc_profile_end synchronises and returns one
- * record per kernel (template instantiation). */
+/* Per-kernel instrumentation (bench.py's roofline).  HIP events cannot be recorded inside a captured
+ * graph (ROCm 7.2), so while enabled every kernel of every `sample_every`-th wavefront / raster step is
+ * captured with a timing slot: its workgroups stamp the earliest start and latest end on the GPU's
+ * constant 100 MHz clock (s_memrealtime), per XCD.  The launch's algorithmic FLOPs and bytes are recorded
+ * at capture.  lbc_profile_begin zeroes every slot; lbc_profile_end synchronises and returns one record
+ * per kernel family from the launches executed since then (the last replay of each sampled graph). */
 typedef struct {
     char name[40];
     long long launches;   /* sampled launches */
     long long total_launches; /* all launches of this kernel since lbc_profile_begin */
-    double total_ms;      /* summed event-to-event durations */
+    double total_ms;      /* summed in-kernel spans (first workgroup start -> last workgroup end) */
     double flops;         /* summed algorithmic FLOPs (2 * rows * K_live * N for a GEMM) */
     double bytes;         /* summed algorithmic bytes (weights + A rows + outputs read/written once) */
+    long long launches_chain; /* sampled launches whose predecessor in the stream chain was sampled too */
+    double total_ms_chain;    /* summed launch-to-launch periods end(previous launch) -> end(this launch):
+                                 the span plus the kernel boundary in front of it */
 } lbc_kernel_stat;
 
 int lbc_profile_begin(lbc_model *m, int sample_every);

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,9 @@
 namespace lbic {
 
 static thread_local std::string g_err;
+// graph captures of different handles are serialised (one-off cost): concurrent first-time captures from
+// several host threads failed a kernel launch under rocprofv3's tracer
+static std::mutex g_capture_mu;
 
 int set_error(int code, const std::string& msg) {
     g_err = msg;
@@ -73,8 +77,11 @@ constexpr int kRanges = 6;        // 0 encoder graph, 1..4 raster decoder lanes,
 struct Prof {
     int sample_every = 0;
     bool active = false;          // current step is sampled
-    struct Rec { int cls; int slot; double flops, bytes; };
+    // prev: slot of the launch before this one in the same sampled step of the same stream chain (-1: none),
+    // so lbc_profile_end can also report the launch-to-launch period end(prev) -> end(this)
+    struct Rec { int cls; int slot; double flops, bytes; int prev; };
     std::vector<Rec> recs;
+    int last_slot = -1;
     unsigned long long* slots = nullptr;   // device, kRanges ranges
     int range = 0, next = 0;               // slot allocation inside the range being captured
     long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
@@ -82,6 +89,15 @@ struct Prof {
     unsigned long long* take() {
         if (!slots || next >= kSlotsPerRange) return nullptr;
         return slots + kSlotU64 * ((size_t)range * kSlotsPerRange + next++);
+    }
+    void step(bool on) {          // a new wavefront / raster step starts (sampled or not)
+        active = on;
+        last_slot = -1;
+    }
+    void add(int cls, const unsigned long long* ts, double flops, double bytes) {
+        const int slot = (int)((ts - slots) / kSlotU64);
+        recs.push_back({cls, slot, flops, bytes, last_slot});
+        last_slot = slot;
     }
 };
 static const char* kKernelNames[] = {"k_gemm_s", "k_gemm", "k_rans_decode", "k_copy_interior"};
@@ -347,14 +363,13 @@ int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     GemmArgs g = g0;
     g.ts = p->take();
     if (!g.ts) return launch_gemm(g0, s);
-    const int slot = (int)((g.ts - p->slots) / kSlotU64);
     int cls = 0;
     int rc = launch_gemm(g, s, &cls);
     if (rc) return rc;
     const double K = k_live > 0 ? k_live : g.K;
     const double flops = 2.0 * g.M * K * g.N;
     const double bytes = 4.0 * (K * g.N + (double)g.M * K + (double)g.M * g.N * (g.square_a ? 2 : 1));
-    p->recs.push_back({cls, slot, flops, bytes});
+    p->add(cls, g.ts, flops, bytes);
     return LBC_OK;
 }
 
@@ -396,30 +411,31 @@ int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, siz
         x0[i] = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
     }
     int rc;
+    // every allocation before the first queued copy: an error return below must not leave copies in flight
+    // that read the local host arrays or the caller's borrowed buffers
     if (total > m->words.bytes && (rc = m->words.alloc(total + total / 2 + (1 << 20)))) return rc;
-    // each stream straight from the caller's buffer to its word offset: no host-side concatenation (a ganged
-    // pass uploads ~1 GB: allocating, zeroing and filling a host copy of it sat on the decoder's critical
-    // path, and one ~1 GB pageable copy crashed rocprofv3 7.2's kernel trace).  (A page-locked staging buffer
-    // here corrupted the stamp slots of the other codec handle's encoder graph on ROCm 7.2 -- a reproducible,
-    // unexplained interaction; pageable copies are kept.)
-    // stream-ordered on the decoder's stream: the words are rewritten only after that stream's previous
-    // graph (which reads them) has drained, whatever the stream's blocking flags
-    for (size_t i = 0; i < n; ++i)
-        HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(m->words.p) + (size_t)base[i] * 4, subs[i].first, subs[i].second,
-                              hipMemcpyHostToDevice, s));
     // per-stream arrays: sized by the stream count, pointers kept stable for the graphs
     const size_t cap = std::max<size_t>(n, 64);
     if ((rc = m->word_base.alloc(cap * sizeof(long long))) || (rc = m->word_count.alloc(cap * sizeof(int))) ||
         (rc = m->st_x.alloc(cap * sizeof(unsigned long long))) || (rc = m->st_ptr.alloc(cap * sizeof(int))) ||
         (rc = m->st_status.alloc(cap * sizeof(int))))
         return rc;
-    HIPCHK(hipMemcpyAsync(m->word_base.p, base.data(), n * sizeof(long long), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(m->word_count.p, cnt.data(), n * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(m->st_x.p, x0.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(m->st_ptr.p, ptr.data(), n * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(m->st_status.p, 0, n * sizeof(int), s));
-    // the host arrays above are locals and the caller's buffers are only borrowed: drain before returning
-    HIPCHK(hipStreamSynchronize(s));
+    // each stream straight from the caller's buffer to its word offset (no host-side concatenation),
+    // stream-ordered on the decoder's stream: the words are rewritten only after that stream's previous
+    // graph (which reads them) has drained, whatever the stream's blocking flags.  The local arrays and the
+    // borrowed buffers stay alive until the synchronisation below, on the error path as well.
+    hipError_t e = hipSuccess;
+    for (size_t i = 0; i < n && e == hipSuccess; ++i)
+        e = hipMemcpyAsync(static_cast<uint8_t*>(m->words.p) + (size_t)base[i] * 4, subs[i].first, subs[i].second,
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->word_base.p, base.data(), n * sizeof(long long), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->word_count.p, cnt.data(), n * sizeof(int), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->st_x.p, x0.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->st_ptr.p, ptr.data(), n * sizeof(int), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(m->st_status.p, 0, n * sizeof(int), s);
+    const hipError_t es = hipStreamSynchronize(s);      // always: drains whatever was queued
+    if (e != hipSuccess) return set_error(LBC_E_HIP, std::string("bitstream upload: ") + hipGetErrorString(e));
+    if (es != hipSuccess) return set_error(LBC_E_HIP, std::string("bitstream upload sync: ") + hipGetErrorString(es));
     return LBC_OK;
 }
 
@@ -748,6 +764,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
                                         (long long)m->table_dev.p, m->prof.sample_every, flags,
                                         m->enc_lds_floor};
     if (!m->enc_exec || key != m->enc_key) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
         if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
         HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
         int crc = prof_range_begin(&m->prof, 0, m->cap);
@@ -757,7 +774,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         for (size_t t = 0; t < m->step_off.size(); ++t)
             if (m->step_cnt[t] > m->lane[0].rows) crc = set_error(LBC_E_STATE, "encoder workspace too small");
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
-            m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
+            m->prof.step(m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0);
             GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), n_img, Hb, Wb);
             if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad);
             if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
@@ -887,6 +904,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
                                         (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
                                         (long long)m->st_x.p, m->prof.sample_every};
     if ((int)m->dec_exec.size() != G || key != m->dec_key) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
         for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
         m->dec_exec.clear();
         g_prof = &m->prof;
@@ -917,7 +935,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             int crc = prof_range_begin(&m->prof, 1 + l, m->cap);
             drop_recs(m->prof, 1 + l);
             for (int h = 0; h < Wb && !crc; ++h) {
-                m->prof.active = m->prof.sample_every > 0 && (h % m->prof.sample_every) == 0;
+                m->prof.step(m->prof.sample_every > 0 && (h % m->prof.sample_every) == 0);
                 const int4* blocks = m->blocks_dec.as<int4>() + (size_t)h * n_img + g0[l];
                 GemmArgs g = base_args(m, blocks, rows, nullptr, n_img, Hb, Wb);
                 g.ctr = r.ctr;
@@ -933,7 +951,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
                 if (!crc && r.ts) {
                     // algorithmic bytes: the CDF tables staged into LDS + idx/mean in + y_qnt out
                     const double b = (double)m->total16 * 2 * ((rows + 7) / 8) + 12.0 * rows * m->M;
-                    m->prof.recs.push_back({2, (int)((r.ts - m->prof.slots) / kSlotU64), 0.0, b});
+                    m->prof.add(2, r.ts, 0.0, b);
                 }
                 if (!crc) crc = run_dec(m, w, g, m->cap);
             }
@@ -1039,6 +1057,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
                                         (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
                                         (long long)m->st_x.p, m->prof.sample_every};
     if (!m->wf_exec || key != m->wf_key) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
         if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
         Work& w = m->lane[0];
         HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
@@ -1047,7 +1066,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
         const int4* blocks = m->blocks_enc.as<int4>();
         g_prof = &m->prof;
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
-            m->prof.active = m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0;
+            m->prof.step(m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0);
             const int rows = m->step_cnt[t];
             GemmArgs g = base_args(m, blocks + m->step_off[t], rows, nullptr, n_img, Hb, Wb);
             crc = run_ctx(m, w, g, true, m->cap);
@@ -1063,7 +1082,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
             if (!crc) crc = launch_rans_decode(r, m->cap);
             if (!crc && r.ts) {
                 const double b = (double)m->total16 * 2 * ((rows + 7) / 8) + 12.0 * rows * m->M;
-                m->prof.recs.push_back({2, (int)((r.ts - m->prof.slots) / kSlotU64), 0.0, b});
+                m->prof.add(2, r.ts, 0.0, b);
             }
             if (!crc) crc = run_dec(m, w, g, m->cap);
         }
@@ -1100,10 +1119,18 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
                     (void*)(p.slots + kSlotU64 * (size_t)kSlotsPerRange * kRanges));
     }
     // sample_every is part of the graph keys: a change re-captures (and re-creates the sample records);
-    // an unchanged value only restarts the launch counting
+    // an unchanged value only restarts the launch counting.  Every stamp slot is zeroed here, so a graph
+    // that is not replayed after this call (a warmup graph, another handle's idle pass) contributes no
+    // sample: lbc_profile_end counts only launches executed since lbc_profile_begin.
     if (sample_every != p.sample_every) p.recs.clear();
     p.sample_every = sample_every;
     for (auto& r : p.replays) r = 0;
+    if (p.slots) {
+        HIPCHK(hipSetDevice(m->cfg.device));
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemset(p.slots, 0, 8 * kSlotU64 * (size_t)kSlotsPerRange * kRanges));
+        HIPCHK(hipDeviceSynchronize());
+    }
     return LBC_OK;
 }
 
@@ -1119,6 +1146,14 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
         HIPCHK(hipDeviceSynchronize());
         std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * kRanges);
         HIPCHK(hipMemcpy(h.data(), p.slots, h.size() * 8, hipMemcpyDeviceToHost));
+        // latest end stamp of a slot over the XCDs (0: not executed since the last reset)
+        auto last_end = [&](int slot) -> unsigned long long {
+            const unsigned long long* t = h.data() + kSlotU64 * (size_t)slot;
+            unsigned long long e = 0;
+            for (int x = 0; x < 8; ++x)
+                if (t[2 * x] && t[2 * x + 1]) e = std::max(e, t[2 * x + 1]);
+            return e;
+        };
         for (const auto& r : p.recs) {
             const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;
             long long span = -1;
@@ -1126,6 +1161,13 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
                 if (!t[2 * x] || !t[2 * x + 1]) continue;
                 const long long d = (long long)(t[2 * x + 1] - (~0ull - t[2 * x]));
                 if (d >= 0 && d > span) span = d;
+            }
+            if (span >= 0 && r.prev >= 0) {    // launch-to-launch period in the stream chain
+                const unsigned long long e0 = last_end(r.prev), e1 = last_end(r.slot);
+                if (e0 && e1 > e0 && e1 - e0 < 100000000ull) {
+                    acc[r.cls].launches_chain += 1;
+                    acc[r.cls].total_ms_chain += (double)(e1 - e0) * 1e-5;
+                }
             }
             if (getenv("LBIC_DEBUG_STAMPS") && span > 10000000) {
                 fprintf(stderr, "handle %p bad slot %d cls %d:", (void*)m, r.slot, r.cls);

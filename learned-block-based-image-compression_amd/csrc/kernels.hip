@@ -18,12 +18,18 @@
 #include "kernels.h"
 
 #include <cmath>
+#include <string>
 
 #include "lbic_internal.h"
 
 namespace lbic {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+static int launch_status(const char* what) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, std::string(what) + " launch failed: " + hipGetErrorString(e));
+}
 
 // Launch-span stamps for sampled launches (bench.py's per-kernel roofline).  HIP events cannot be
 // recorded inside a captured graph on ROCm 7.2, so the kernels stamp themselves on the constant 100 MHz
@@ -517,17 +523,17 @@ template <int BM, int BN, int NW, int CH>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "LDS request above 160 KB");
-    static bool attr = false;
-    if (!attr) {
+    static const bool attr = [] {     // once per instantiation (thread-safe static initialisation)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        return true;
+    }();
+    (void)attr;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     GemmArgs gs = g;
     gs.swz = g_enc_swz;
     hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH>), grid, dim3(NW * 64), lds, s, gs);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm launch failed");
+    return launch_status("k_gemm");
 }
 
 int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
@@ -587,7 +593,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
                 else LBIC_V(13, false, false);
 #undef LBIC_V
         }
-        return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_gemm_s launch failed");
+        return launch_status("k_gemm_s");
     }
     if (cfg_id) *cfg_id = 1;
     // Encoder wavefront steps (n_img images x up to 48 blocks): many small tiles beat few large ones
@@ -835,15 +841,15 @@ int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
     if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 tables must be padded to 16 bytes");
     const size_t lds = (size_t)a.total16 * sizeof(uint16_t) + (size_t)RANS_WPB * RANS_WIN * sizeof(uint32_t);
-    static bool attr = false;
-    if (!attr) {
+    static const bool attr = [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+        return true;
+    }();
+    (void)attr;
     const int wpb = a.rows < RANS_WPB ? a.rows : RANS_WPB;
     hipLaunchKernelGGL(k_rans_decode, dim3((a.rows + RANS_WPB - 1) / RANS_WPB), dim3(wpb * 64), lds, s, a);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "k_rans_decode launch failed");
+    return launch_status("k_rans_decode");
 }
 
 __global__ void k_ctr_add(int* c, int d) { *c += d; }
@@ -858,12 +864,12 @@ __global__ void k_zero_u64(unsigned long long* p, int n) {
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s) {
     if (n <= 0) return LBC_OK;
     hipLaunchKernelGGL(k_zero_u64, dim3((n + 255) / 256), dim3(256), 0, s, p, n);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "zero launch failed");
+    return launch_status("zero");
 }
 
 int launch_ctr_add(int* ctr, int d, hipStream_t s) {
     hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, s, ctr, d);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "ctr launch failed");
+    return launch_status("ctr");
 }
 
 __global__ void k_copy_interior(const float* __restrict__ zpad, float* __restrict__ zout, int n_img, int Hb, int Wb,
@@ -902,14 +908,14 @@ int launch_fill_interior(const float* zin, float* zpad, int n_img, int Hb, int W
     const long total = (long)n_img * Hb * Wb * Cx / 4;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(k_fill_interior, dim3(blocks), dim3(256), 0, s, zin, zpad, n_img, Hb, Wb, Cx);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "fill launch failed");
+    return launch_status("fill");
 }
 
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s) {
     const long total = (long)n_img * Hb * Wb * Cx / 4;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(k_copy_interior, dim3(blocks), dim3(256), 0, s, zpad, zout, n_img, Hb, Wb, Cx);
-    return hipGetLastError() == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, "copy launch failed");
+    return launch_status("copy");
 }
 
 }  // namespace lbic

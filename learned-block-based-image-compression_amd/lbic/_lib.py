@@ -19,7 +19,8 @@ LBC_E_NOT_UPDATED = -4
 class LbcKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_longlong), ("total_launches", ctypes.c_longlong),
                 ("total_ms", ctypes.c_double),
-                ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+                ("flops", ctypes.c_double), ("bytes", ctypes.c_double),
+                ("launches_chain", ctypes.c_longlong), ("total_ms_chain", ctypes.c_double)]
 
 
 class LbcConfig(ctypes.Structure):

@@ -263,16 +263,19 @@ class BlockBasedImgCompLossyNetv9:
     __call__ = forward
 
     def profile_begin(self, sample_every: int):
-        """Sample every n-th step's kernels with HIP events (lbc_profile_begin)."""
+        """Sample every n-th step's kernels with in-kernel timing stamps (lbc_profile_begin)."""
         _lib.check(_lib.lib().lbc_profile_begin(self._h, int(sample_every)))
 
     def profile_end(self):
-        """-> {kernel name: dict(launches, total_ms, flops, bytes)} for the sampled launches."""
+        """-> {kernel family: dict(launches, total_launches, total_ms, flops, bytes, launches_chain,
+        total_ms_chain)} over the sampled launches executed since profile_begin."""
         arr = (_lib.LbcKernelStat * 8)()
         n = ctypes.c_int()
         _lib.check(_lib.lib().lbc_profile_end(self._h, arr, 8, ctypes.byref(n)))
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_launches=arr[i].total_launches,
-                                           total_ms=arr[i].total_ms, flops=arr[i].flops, bytes=arr[i].bytes)
+                                           total_ms=arr[i].total_ms, flops=arr[i].flops, bytes=arr[i].bytes,
+                                           launches_chain=arr[i].launches_chain,
+                                           total_ms_chain=arr[i].total_ms_chain)
                 for i in range(n.value)}
 
     def last_timing(self):

@@ -14,6 +14,12 @@ trainable tensor from ``numpy.random.default_rng(seed)`` in the reference's stat
   ``NonNegativeParametrizer.init`` (utils/parametrizers.py:42-43) so that the forward reparam
   (:45-47) gives back beta_eff / gamma_eff.
 
+``rate="low"`` draws the same tensors and re-scales them to the B8_lowrate operating point (about
+0.12-0.14 bpp on uniform-noise frames, BASELINE.md: the published B8_lowrate point is 0.117 bpp): small
+latents (``LOW_Y_GAIN``), a context net whose scale channels mostly sit at the bottom of the scale
+table with a few wide ones (bias exp(-2.6 + 3.6 (i/(M-1))^18)), weak mean prediction.  Almost every
+symbol is 0, as in a trained low-rate model, which is the regime the rANS decoder sees on that config.
+
 The same function feeds the reference (golden generation), the oracle, the HIP library and bench.py,
 so all of them see identical weights for a seed.
 """
@@ -31,9 +37,17 @@ Y_GAIN = 8.0
 XHAT_GAIN = 0.6
 YQ_GAIN = 0.12
 MEAN_GAIN = 0.5
+# rate="low" (B8_lowrate operating point)
+LOW_Y_GAIN = 0.4
+LOW_SCALE_GAIN = 0.3
+LOW_MEAN_GAIN = 0.1
+LOW_SCALE_POW = 18.0
 
 
-def synth_state_dict(arch: Arch, seed: int = 1337) -> Dict[str, np.ndarray]:
+def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high") -> Dict[str, np.ndarray]:
+    if rate not in ("high", "low"):
+        raise ValueError(f"rate must be 'high' or 'low', not {rate!r}")
+    low = rate == "low"
     rng = np.random.default_rng(seed)
     out: Dict[str, np.ndarray] = {}
     convs = {c[0]: c for c in arch.conv_specs()}
@@ -44,19 +58,23 @@ def synth_state_dict(arch: Arch, seed: int = 1337) -> Dict[str, np.ndarray]:
             live = cin * (4 if (k == 3 and mtype == "A") else 5 if k == 3 else 1)
             w = rng.standard_normal(shape, dtype=np.float32) * np.float32(1.0 / math.sqrt(live))
             if mod == "prtr_forward3.5":
-                w *= np.float32(Y_GAIN)
+                w *= np.float32(LOW_Y_GAIN if low else Y_GAIN)
             if mod == "prtr_inverse1":
                 w *= np.float32(YQ_GAIN)
             if mod == "prtr_inverse3.5":
                 w *= np.float32(XHAT_GAIN)
             if mod == "get_meanscale.6":
-                w[: arch.M] *= np.float32(1.5)            # scale channels: spread around the bias
-                w[arch.M:] *= np.float32(MEAN_GAIN)        # mean channels
+                w[: arch.M] *= np.float32(LOW_SCALE_GAIN if low else 1.5)   # scale channels around the bias
+                w[arch.M:] *= np.float32(LOW_MEAN_GAIN if low else MEAN_GAIN)   # mean channels
             out[name] = w
         elif leaf == "bias":
             b = (rng.standard_normal(shape, dtype=np.float32) * np.float32(0.05))
             if mod == "get_meanscale.6":
-                b[: arch.M] = np.exp(np.linspace(-2.0, 5.0, arch.M)).astype(np.float32)
+                if low:
+                    t = np.arange(arch.M, dtype=np.float64) / max(arch.M - 1, 1)
+                    b[: arch.M] = np.exp(-2.6 + 3.6 * t ** LOW_SCALE_POW).astype(np.float32)
+                else:
+                    b[: arch.M] = np.exp(np.linspace(-2.0, 5.0, arch.M)).astype(np.float32)
             out[name] = b
         elif leaf == "beta":
             beta_eff = rng.uniform(0.5, 1.5, size=shape).astype(np.float32)

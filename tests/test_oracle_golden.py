@@ -136,3 +136,20 @@ def test_oracle_validate_recu_matches_reference(name):
     z, info = codec.validate_recu(g["x"])
     assert np.abs(z - g["zhat"]).max() < 1e-5
     assert (np.abs(info - g["self_info"]) <= 1e-4 * np.maximum(1.0, np.abs(g["self_info"]))).all()
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "tiny_ks3311"])
+def test_torch_cpu_restatement_matches_reference(name):
+    """oracle/torch_ref.py (bench.py's CPU baseline) reproduces the reference's closed loop bit-exactly on the
+    tie-screened fixtures, and its decoder inverts its encoder."""
+    import torch
+    from oracle.torch_ref import TorchRef
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    torch.set_num_threads(1)
+    t = TorchRef(arch, synth_state_dict(arch, int(g["weight_seed"])))
+    r = t.compress(g["x"])
+    assert np.array_equal(r["symbols"], g["symbols"])
+    assert np.array_equal(r["indexes"], g["indexes"])
+    assert np.abs(r["zhat"] - g["zhat"]).max() < 1e-5
+    assert np.array_equal(t.decompress(r["bytes"], *g["x"].shape[:2]), r["zhat"])

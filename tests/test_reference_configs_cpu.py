@@ -1,0 +1,98 @@
+"""The reference's own four configs (/root/reference/configs/*.json, read verbatim; only ``valid_data`` is
+redirected to a local PNG folder) through this repository's main.py: JSON parsing, the multi-lambda sweep
+(main.py:17-27 of the reference), process_config's experiment layout (utils/config.py:69-102), agent
+dispatch by name and the agent's construction up to the device check, which on this GPU-less host must be
+the loud "no GPU" error (no CPU fallback).  The same flow runs end to end on the GPU in
+tests/test_agent_gpu.py.  Skipped where /root/reference is absent (the GPU box).
+
+Also: bench.py's multi-GPU launcher and its per-image record gather (gloo, world size 2)."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+REF_CONFIGS = sorted(glob.glob("/root/reference/configs/*.json"))
+
+
+@pytest.mark.skipif(not REF_CONFIGS, reason="reference configs not present (GPU box)")
+@pytest.mark.parametrize("path", REF_CONFIGS, ids=[os.path.basename(p) for p in REF_CONFIGS])
+def test_reference_config_runs_through_main(path, tmp_path, monkeypatch):
+    from PIL import Image
+    import main as lbic_main
+    from lbic.arch import arch_from_config
+    from lbic.config import AttrDict
+    raw = json.load(open(path))
+    data = tmp_path / "valid"
+    data.mkdir()
+    Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(data / "a.png")
+    cfg = dict(raw)
+    cfg["valid_data"] = str(data)                       # the only override
+    assert set(cfg) == set(raw)
+    p = tmp_path / os.path.basename(path)
+    p.write_text(json.dumps(cfg))
+    monkeypatch.chdir(tmp_path)
+    arch = arch_from_config(AttrDict(cfg))
+    assert (arch.B, list(arch.KS), arch.N, arch.M) == (raw["block_size"], raw["KS"], raw["N"], raw["M"])
+    seen = []
+    real = lbic_main.AGENTS["BlockBasedImgCompLossyAgent"]
+
+    class Probe(real):
+        def __init__(self, config):
+            seen.append((config.exp_name, config.lambda_, config.mode, config.log_dir))
+            super().__init__(config)            # -> the device check (no GPU here)
+
+    monkeypatch.setitem(lbic_main.AGENTS, "BlockBasedImgCompLossyAgent", Probe)
+    with pytest.raises(RuntimeError, match="no GPU is visible"):
+        lbic_main.main([str(p)])
+    lam = raw["lambda_"][0] if raw.get("multi_agent") else raw["lambda_"]
+    exp, got_lam, mode, log_dir = seen[0]
+    assert got_lam == lam and mode == raw["mode"]
+    if raw.get("multi_agent"):
+        assert exp == os.path.join(raw["multi_exp_name"], "exp_" + str(lam))
+    # (logging is set up once per process, as the reference's run_once setup_logging, utils/config.py:24)
+    assert all(os.path.isdir(os.path.join(log_dir, "..", d)) for d in ("summaries", "checkpoints", "out", "logs"))
+
+
+def test_bench_relaunch_command(monkeypatch):
+    """--gpus N without WORLD_SIZE re-runs bench.py under torch.distributed.run (one process per GPU, 127.0.0.1)
+    as a child process and exits with its code."""
+    import sys
+    import bench
+    calls = []
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd: calls.append(cmd) or 7)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    args = bench.parse_args()
+    assert bench.relaunch_distributed(args) == 7
+    cmd = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def _gather_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rec = torch.tensor([[100.0 + rank, 5.0 * rank, 12.0], [200.0 + rank, 1.0, 12.0]], dtype=torch.float64)
+    allrec, ok = bench.gather_records(rec, rank != 7, True)
+    if rank == 0:
+        np.save(out, allrec.numpy())
+        assert ok
+    dist.destroy_process_group()
+
+
+def test_bench_gather_records_gloo(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rec.npy")
+    mp.spawn(_gather_worker, args=(2, port, out), nprocs=2, join=True)
+    rec = np.load(out)
+    assert rec.shape == (4, 3)
+    assert list(rec[:, 0]) == [100.0, 200.0, 101.0, 201.0]
