@@ -527,24 +527,32 @@ def compare_full_frame_fixture(model, args, arch, dev):
     g = dict(np.load(path))
     if str(g["rate"]) != args.rate:
         return None
-    x = torch.from_numpy(g["x"])[None].to(dev)
-    r = model.compress_batch(x, want_bits=True)
+    import hashlib
+    from lbic.layout import image_to_blocks
+    H, W = int(g["H"]), int(g["W"])
+    img = np.random.default_rng(int(g["image_seed"])).integers(0, 256, (1, 3, H, W), dtype=np.uint8)[0]
+    if hashlib.sha256(img.tobytes()).hexdigest() != str(g["image_sha256"]):
+        return dict(error="fixture frame regeneration differs")
+    xb = image_to_blocks(img.astype(np.float32) / 255.0 - 0.5, arch.B)
+    r = model.compress_batch(torch.from_numpy(xb)[None].to(dev), want_bits=True)
     torch.cuda.synchronize(dev)
     sym = r["symbols"][0].cpu().numpy()
     idx = r["indexes"][0].cpu().numpy()
     zh = r["zhat"][0].cpu().numpy()
-    bits = r["bits"][0].cpu().numpy()
-    H, W = g["image"].shape[1:]
-    x0 = g["x"].astype(np.float64)
-
-    def psnr(z):
-        return float(-10 * np.log10(np.mean((z.astype(np.float64) - x0) ** 2)))
-    zref = g["zhat"]
-    return dict(fixture="tests/golden/frame_b8_lowrate.npz (reference closed loop, one 768x768 frame)",
-                symbol_mismatches=int((sym != g["symbols"]).sum()), index_mismatches=int((idx != g["indexes"]).sum()),
-                symbols=int(sym.size), zhat_max_abs_diff=float(np.abs(zh - zref).max()),
-                psnr_db=round(psnr(zh), 5), psnr_ref_db=round(psnr(zref), 5),
-                est_bpp=round(float(bits.sum()) / (H * W), 6), est_bpp_ref=round(float(g["bits"].sum()) / (H * W), 6))
+    bits = r["bits"][0].cpu().numpy().astype(np.float64)
+    rows = g["zhat_rows"]
+    mse = float(np.mean((zh.astype(np.float64) - xb) ** 2))
+    est = float(bits.sum()) / (H * W)
+    est_ref = float(g["bits_per_block"].sum()) / (H * W)
+    psnr, psnr_ref = -10 * np.log10(mse), float(g["psnr_db"])
+    return dict(fixture="tests/golden/frame_b8_lowrate.npz: the reference's compress() closed loop on one 768x768 frame "
+                        "(graphs/models/BlockBasedImgCompLossy_net.py:319-361), same weights and frame",
+                symbols=int(sym.size), symbol_mismatches=int((sym != g["symbols"]).sum()),
+                index_mismatches=int((idx != g["indexes"].astype(np.int32)).sum()),
+                zhat_rows_max_abs_diff=float(np.abs(zh[rows] - g["zhat_row_data"]).max()),
+                zhat_block_sum_max_abs_diff=float(np.abs(zh.astype(np.float64).sum(-1) - g["zhat_block_sum"]).max()),
+                psnr_db=round(psnr, 6), psnr_ref_db=round(psnr_ref, 6), psnr_rel_diff=float(abs(psnr - psnr_ref) / psnr_ref),
+                est_bpp=round(est, 7), est_bpp_ref=round(est_ref, 7), est_bpp_rel_diff=float(abs(est - est_ref) / est_ref))
 
 
 if __name__ == "__main__":

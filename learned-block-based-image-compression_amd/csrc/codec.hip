@@ -439,6 +439,17 @@ int upload_streams(lbc_model* m, const std::vector<std::pair<const uint8_t*, siz
     return LBC_OK;
 }
 
+int rans_sparse_choice(const size_t* lens, int n, double symbols) {
+    if (const char* e = getenv("LBIC_RANS_SPARSE")) return atoi(e) ? 1 : 0;
+    static const double thr = [] {
+        const char* e = getenv("LBIC_RANS_SPARSE_BPS");
+        return e ? atof(e) : 1.0;
+    }();
+    double bytes = 0;
+    for (int i = 0; i < n; ++i) bytes += (double)lens[i];
+    return symbols > 0 && 8.0 * bytes / symbols < thr ? 1 : 0;
+}
+
 int check_status(lbc_model* m, size_t n, hipStream_t s) {
     std::vector<int> status(n);
     HIPCHK(hipMemcpyAsync(status.data(), m->st_status.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -866,6 +877,8 @@ int lbc_rans_decode_gpu(lbc_model* m, const uint8_t* const* streams, const size_
     if ((rc = upload_streams(m, subs, s))) return rc;
     RansArgs r = rans_args(m);
     r.rows = n_streams;
+    double nsym = (double)n_streams * n_chunks * m->M;
+    r.sparse = rans_sparse_choice(lens, n_streams, nsym);
     for (int c = 0; c < n_chunks && !rc; ++c) {
         r.idx = idx_dev + (size_t)c * n_streams * m->M;
         r.sym_out = sym_dev + (size_t)c * n_streams * m->M;
@@ -900,9 +913,12 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     int g0[kLanes + 1];
     for (int l = 0; l <= G; ++l) g0[l] = l * n_img / G;
     if ((rc = m->ctr.alloc(kLanes * sizeof(int)))) return rc;
+    // rANS decoder variant: the sparse one (centre-interval fast path, no LDS table image) when the streams
+    // average under LBIC_RANS_SPARSE_BPS bits per symbol (default 1.0; LBIC_RANS_SPARSE=0/1 forces it)
+    int sparse = rans_sparse_choice(lens, n_img, (double)n_img * Hb * Wb * m->M);
     const std::vector<long long> key = {n_img, Hb, Wb, G, (long long)m->words.p, (long long)m->zpad.p,
                                         (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
-                                        (long long)m->st_x.p, m->prof.sample_every};
+                                        (long long)m->st_x.p, m->prof.sample_every, sparse};
     if ((int)m->dec_exec.size() != G || key != m->dec_key) {
         std::lock_guard<std::mutex> lk(g_capture_mu);
         for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
@@ -931,6 +947,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             r.rows = rows;
             r.ctr = m->ctr.as<int>() + l;
             r.ctr_stride = Wb * n_img;
+            r.sparse = sparse;
             HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
             int crc = prof_range_begin(&m->prof, 1 + l, m->cap);
             drop_recs(m->prof, 1 + l);
@@ -1053,9 +1070,12 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
     // the whole anti-diagonal wavefront (the encoder's schedule) as one graph: per step, context net of
     // every block on the diagonal -> one wave per (image, block row) decodes that row's next block ->
     // decoder transform of every block
+    std::vector<size_t> sub_lens;
+    for (const auto& sb : subs) sub_lens.push_back(sb.second);
+    const int sparse = rans_sparse_choice(sub_lens.data(), (int)sub_lens.size(), (double)n_img * Hb * Wb * m->M);
     const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->words.p, (long long)m->zpad.p,
                                         (long long)m->lane[0].ctx0.p, (long long)m->table_dev.p,
-                                        (long long)m->st_x.p, m->prof.sample_every};
+                                        (long long)m->st_x.p, m->prof.sample_every, sparse};
     if (!m->wf_exec || key != m->wf_key) {
         std::lock_guard<std::mutex> lk(g_capture_mu);
         if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
@@ -1077,6 +1097,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
             r.rows = rows;
             r.blocks = blocks + m->step_off[t];
             r.streams_per_img = Hb;
+            r.sparse = sparse;
             r.ts = m->prof.active ? m->prof.take() : nullptr;
             m->prof.per_replay[kRanges - 1][2] += 1;
             if (!crc) crc = launch_rans_decode(r, m->cap);

@@ -74,8 +74,9 @@ struct GemmArgs {
 struct RansArgs {
     const uint16_t* cdf16;   // LDS image of the tables (build_rans_gpu_tables: coarse rows, then padded
                              // fine rows, entries stored as cdf - 1)
-    const int* tmeta;        // [5][64] per table: fine row start, 2 S (S = symbols per coarse lane), cdf_length - 2,
-                             // coarse row start (starts in bytes of the image), offset (-pmf_center)
+    const int* tmeta;        // [6][64] per table: fine row start, 2 S (S = symbols per coarse lane), cdf_length - 2,
+                             // coarse row start (starts in bytes of the image), offset (-pmf_center), centre
+                             // interval of the value-0 symbol packed lo | freq << 16
     int total16;             // entries in cdf16 (multiple of 8)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;
@@ -95,6 +96,7 @@ struct RansArgs {
     unsigned long long* ts;
     int rows;
     int streams_per_img;     // 1: one stream per image (reference format); Hb: one per block row (sub-stream format)
+    int sparse;              // 1: k_rans_decode_sparse (centre-interval fast path, tables read from global memory)
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm

@@ -827,6 +827,142 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     RSTAMP(3);
 }
 
+// Sparse variant (low rates: almost every symbol is the most probable one, value 0).  No table image in LDS:
+// per symbol ONE compare of cum against the centre interval [lo, lo + freq) of the symbol's table (tmeta row
+// 5, gathered into a lane-per-symbol register in the prologue) decides; a hit costs the 64-bit state update
+// and nothing else.  A miss runs the two-level search of rans_row on the table image in global memory (the
+// 70 KB image stays L2-resident: every launch of every decoder reads it).  The prologue therefore needs only
+// the stream state, the block's indexes and the stream words -- no 70 KB LDS fill and no workgroup barrier
+// for it -- and each wave is independent.  Bit-identical to rans_row (same coder, same tables).
+__device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane) {
+    const bool valid = row_in < a.rows;
+    const int row = valid ? row_in : a.rows - 1;
+    int img = row;
+    if (a.streams_per_img > 1) {
+        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
+        const int4 blk = blocks[row];
+        img = blk.x * a.streams_per_img + blk.y;
+    }
+    img = __builtin_amdgcn_readfirstlane(img);
+    const int Mlat = a.Mlat;
+    const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
+    const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane], t_lf = a.tmeta[320 + lane];
+    const unsigned long long x_in = a.state_x[img];
+    const int p_in = a.state_ptr[img];
+    const long long wb = a.word_base[img];
+    const int nw_in = a.word_count[img];
+    int ti[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) ti[kb] = a.idx[(long)row * Mlat + min(kb * 64 + lane, Mlat - 1)] & 63;
+    unsigned long long x = uni64(x_in);
+    int p = __builtin_amdgcn_readfirstlane(p_in);
+    const uint32_t* w = a.words + wb;
+    const int nw = __builtin_amdgcn_readfirstlane(nw_in);
+    const int p0 = p;
+    {
+        uint32_t wv[RANS_WIN / 64];
+#pragma unroll
+        for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
+#pragma unroll
+        for (int k = 0; k < RANS_WIN / 64; ++k) lwin[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
+    }
+    // lane i of chunk kb = symbol 64 kb + i: its centre interval, table metadata and offset
+    int lf[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int sel = ti[kb] << 2;
+        lf[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lf);
+        sfb[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
+        sS[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
+        slm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
+        sca[kb] = __builtin_amdgcn_ds_bpermute(sel, t_ca);
+        moff[kb] = __builtin_amdgcn_ds_bpermute(sel, t_off);
+        symv[kb] = -moff[kb];            // the centre symbol's index (value 0)
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the window is in LDS (this wave's own writes)
+    __builtin_amdgcn_wave_barrier();
+    if (!valid) return;
+    int bad = 0;
+    int q0 = 0;
+    uint32_t wbuf = lwin[lane];
+    uint32_t wn = rdlane(wbuf, 0);
+    auto renorm = [&]() {
+        uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);   // 0 <=> x < RANS64_L = 2^31
+        asm("" : "+s"(t));
+        if (t == 0) {
+            x = (x << 32) | wn;
+            ++p;
+            if (p - p0 - q0 >= 64) {
+                q0 = min(q0 + 64, RANS_WIN - 64);
+                wbuf = lwin[q0 + lane];
+            }
+            wn = rdlane(wbuf, min(p - p0 - q0, 63));
+        }
+        x = uni64(x);
+    };
+    const uint16_t* img16 = a.cdf16;
+    const int lane2 = lane * 2;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int cnt_i = __builtin_amdgcn_readfirstlane(min(64, Mlat - kb * 64));
+        if (cnt_i <= 0) break;
+        for (int ii = 0; ii < cnt_i; ++ii) {
+            const uint32_t cum = (uint32_t)x & 0xffffu;
+            const uint32_t lfi = rdlane((uint32_t)lf[kb], ii);
+            const uint32_t d = cum - (lfi & 0xffffu), fr = lfi >> 16;
+            if (d < fr) {                               // the most probable symbol (value 0)
+                x = (unsigned long long)fr * (x >> 16) + d;
+                renorm();
+                continue;                               // symv[kb] lane ii already holds the centre index
+            }
+            const int fb = rdlane_i(sfb[kb], ii), S = rdlane_i(sS[kb], ii);
+            const int lm2 = rdlane_i(slm[kb], ii), ca = rdlane_i(sca[kb], ii);
+            const uint32_t cv = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + ca + lane2);
+            const int j = __popcll(__ballot(cv < cum));
+            const int sbb = j * S;
+            const uint32_t fine = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + fb + sbb + lane2);
+            const int kk = __popcll(__ballot(fine < cum) | 1ull) - 1;
+            const int sidx = (sbb >> 1) + kk;
+            const uint32_t start = (rdlane(fine, kk) + 1u) & 0xffffu;
+            const uint32_t nxt = rdlane(fine, kk + 1) + 1u;
+            x = (unsigned long long)(nxt - start) * (x >> 16) + (cum - start);
+            renorm();
+            int v = sidx;
+            if (__builtin_expect(sidx == lm2, 0)) {   // escape: value coded in 4-bit bypass chunks
+                auto get_bits = [&]() -> uint32_t {
+                    const uint32_t b = (uint32_t)(x & 15u);
+                    x >>= 4;
+                    renorm();
+                    return b;
+                };
+                uint32_t cc = get_bits(), nb = cc;
+                while (cc == 15u && nb <= 8) { cc = get_bits(); nb += cc; }
+                if (nb > 8) { bad |= 4; nb = 0; }
+                uint32_t raw = 0;
+                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits() << (jj * 4);
+                v = (int)(raw >> 1);
+                v = (raw & 1) ? -v - 1 : v + lm2;
+            }
+            symv[kb] = lane == ii ? v : symv[kb];
+        }
+    }
+    bad |= p > nw;
+    bad |= (p - p0 > RANS_WIN) ? 8 : 0;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        const int i = kb * 64 + lane;
+        if (i < Mlat) {
+            if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
+            else a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
+        }
+    }
+    if (lane == 0) {
+        a.state_x[img] = x;
+        a.state_ptr[img] = p;
+        if (bad) a.status[img] = bad;
+    }
+}
+
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
     stamp_start(a.ts);
@@ -836,10 +972,23 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
     stamp_end(a.ts);
 }
 
+// one wave per stream, one stream per workgroup: no LDS shared between waves, so nothing to wait for but
+// the wave's own loads
+__global__ __launch_bounds__(64) void k_rans_decode_sparse(const RansArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
+    stamp_start(a.ts);
+    rans_row_sparse(a, lwin, blockIdx.x, threadIdx.x);
+    stamp_end(a.ts);
+}
+
 int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     if (a.rows <= 0) return LBC_OK;     // an empty wavefront step (e.g. odd steps of a one-column frame)
     if (a.Mlat > RANS_MAXLAT) return set_error(LBC_E_ARG, "M > 256 not supported by the GPU rANS decoder");
     if (a.total16 % 8) return set_error(LBC_E_ARG, "cdf16 tables must be padded to 16 bytes");
+    if (a.sparse) {
+        hipLaunchKernelGGL(k_rans_decode_sparse, dim3(a.rows), dim3(64), 0, s, a);
+        return launch_status("k_rans_decode_sparse");
+    }
     const size_t lds = (size_t)a.total16 * sizeof(uint16_t) + (size_t)RANS_WPB * RANS_WIN * sizeof(uint32_t);
     static const bool attr = [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rans_decode),

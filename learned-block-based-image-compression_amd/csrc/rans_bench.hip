@@ -50,12 +50,14 @@ int main(int argc, char** argv) {
     if (build_rans_gpu_tables(t, c16, meta)) return 1;
     const int total16 = (int)c16.size();
     const int lo_idx = argc > 3 ? atoi(argv[3]) : 0, hi_idx = argc > 4 ? atoi(argv[4]) : 63;
-    // symbols: index uniform over the table, value ~ N(0, 1.2 sigma)
+    const int sparse = argc > 5 ? atoi(argv[5]) : 0;            // 1: k_rans_decode_sparse
+    const float spread = argc > 6 ? (float)atof(argv[6]) : 1.2f;   // value ~ N(0, spread sigma): 0.1 = low rate
+    // symbols: index uniform over the table, value ~ N(0, spread sigma)
     std::mt19937 rng(1);
     std::vector<int32_t> idx((size_t)n_img * steps * M), sym(idx.size());
     for (size_t i = 0; i < idx.size(); ++i) {
         idx[i] = lo_idx + (int)(rng() % (hi_idx - lo_idx + 1));
-        std::normal_distribution<float> nd(0.f, t.table[idx[i]] * 1.2f);
+        std::normal_distribution<float> nd(0.f, t.table[idx[i]] * spread);
         sym[i] = (int)std::lrint(nd(rng));
     }
     std::vector<uint32_t> words;
@@ -94,6 +96,8 @@ int main(int argc, char** argv) {
     std::vector<float> ksi((size_t)n_img * 2 * M, 0.f);
     a.ksi = (const float*)up(ksi.data(), ksi.size() * 4);
     a.ldk = 2 * M; a.Mlat = M; a.ldy = M; a.rows = n_img;
+    a.sparse = sparse;
+    size_t nbytes = words.size() * 4;
     float* yq; (void)hipMalloc(&yq, sizeof(float) * n_img * M * steps);
     a.blocks = (const int4*)up(blocks.data(), blocks.size() * sizeof(int4));
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
@@ -126,7 +130,8 @@ int main(int argc, char** argv) {
         printf("cycles (s_memtime): prologue %.0f, loop %.0f (%.0f / symbol), epilogue %.0f\n", t[0], t[1], t[1] / M, t[2]);
     }
 #endif
-    printf("rans decode: %d images x %d symbols, tables %d..%d: %.2f us/step, %.0f ns/symbol, mismatches %ld\n", n_img, M, lo_idx, hi_idx,
+    printf("rans decode (%s): %d images x %d symbols, tables %d..%d, %.3f bits/symbol: %.2f us/step, %.0f ns/symbol, "
+           "mismatches %ld\n", sparse ? "sparse" : "lds", n_img, M, lo_idx, hi_idx, 8.0 * nbytes / idx.size(),
            ms * 1e3 / steps, ms * 1e6 / steps / M, bad);
     return 0;
 }

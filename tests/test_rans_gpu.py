@@ -14,6 +14,14 @@ from test_gpu_parity import model_for
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["lds", "sparse"])
+def rans_variant(request, monkeypatch):
+    """Both decoder variants: the LDS table image (k_rans_decode) and the sparse one (centre-interval fast path,
+    tables read from global memory, k_rans_decode_sparse); lbc_decode picks by bits per symbol."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1" if request.param == "sparse" else "0")
+    return request.param
+
+
 def _symbols(rng, tabs, idx, wide):
     """Gaussian draws at 1.3x the table scale (mostly inside the table), plus `wide` extreme values."""
     scale = np.asarray(tabs.table, np.float64)[idx]
@@ -70,3 +78,20 @@ def test_gpu_decode_truncated_stream_raises():
         m.rans_decode_gpu(streams, torch.from_numpy(idx[:, :1]))
     # the handle still decodes afterwards
     assert np.array_equal(m.rans_decode_gpu(streams, torch.from_numpy(idx)).cpu().numpy(), sym)
+
+
+def test_gpu_decode_low_rate_mostly_centre():
+    """The regime of the B8_lowrate operating point: almost every symbol is the table's centre (value 0), a few
+    +-1 / +-2 and rare escapes, over every table."""
+    M, n = 96, 32
+    m = model_for(Arch(8, (3, 1, 1, 1), 64, M))
+    tabs = O.GaussianTables()
+    rng = np.random.default_rng(11)
+    idx = rng.integers(0, 64, (6, n, M)).astype(np.int32)
+    sym = np.zeros(idx.shape, np.int32)
+    flat = sym.reshape(-1)
+    pos = rng.choice(flat.size, size=flat.size // 50, replace=False)
+    flat[pos] = rng.choice([-2, -1, 1, 2, 3000], size=pos.size)
+    streams = [tabs.encode(sym[:, k].reshape(-1), idx[:, k].reshape(-1)) for k in range(n)]
+    out = m.rans_decode_gpu(streams, torch.from_numpy(idx)).cpu().numpy()
+    assert np.array_equal(out, sym)
