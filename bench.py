@@ -76,8 +76,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget", type=float, default=24.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--side-steps", type=int, default=2,
                     help="batches of the one-decode-in-flight and serial schedules reported beside (0 = skip)")
-    ap.add_argument("--gang", type=int, default=8, help="batches per raster pass of the gang schedule (0 = skip)")
-    ap.add_argument("--substream-steps", type=int, default=2, help="batches in the sub-stream format (0 = skip)")
+    ap.add_argument("--gang", type=int, default=0,
+                    help="batches per raster pass of an extra gang-schedule leg (0 = skip; not in the default run, so "
+                         "the same-command rocprof summary holds only the headline's kernel shapes)")
+    ap.add_argument("--substream-steps", type=int, default=0, help="batches in the opt-in sub-stream format (0 = skip)")
     ap.add_argument("--encode-only", type=int, default=0, help="profiling aid: this many encoder passes, no JSON")
     return ap.parse_args(argv)
 

@@ -835,6 +835,7 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 // the stream state, the block's indexes and the stream words -- no 70 KB LDS fill and no workgroup barrier
 // for it -- and each wave is independent.  Bit-identical to rans_row (same coder, same tables).
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane) {
+    RSTAMP(0);
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
     int img = row;
@@ -882,6 +883,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the window is in LDS (this wave's own writes)
     __builtin_amdgcn_wave_barrier();
     if (!valid) return;
+    RSTAMP(1);
     int bad = 0;
     int q0 = 0;
     uint32_t wbuf = lwin[lane];
@@ -946,6 +948,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
             symv[kb] = lane == ii ? v : symv[kb];
         }
     }
+    RSTAMP(2);
     bad |= p > nw;
     bad |= (p - p0 > RANS_WIN) ? 8 : 0;
 #pragma unroll
@@ -961,6 +964,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         a.state_ptr[img] = p;
         if (bad) a.status[img] = bad;
     }
+    RSTAMP(3);
 }
 
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {

@@ -44,10 +44,12 @@ def main():
         if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
             r["hbm_bytes_per_dispatch"] = (2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024
         res[k] = r
+    res["_source"] = {"dirs": dirs, "note": "per-dispatch means over every dispatch of the profiled command"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
     for k, r in sorted(res.items()):
-        print(k, {c: round(v, 1) for c, v in r.items()})
+        if not k.startswith("_"):
+            print(k, {c: round(v, 1) for c, v in r.items()})
 
 
 if __name__ == "__main__":
