@@ -867,12 +867,14 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
 #pragma unroll
         for (int k = 0; k < RANS_WIN / 64; ++k) lwin[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
     }
-    // lane i of chunk kb = symbol 64 kb + i: its centre interval, table metadata and offset
-    int lf[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
+    // lane i of chunk kb = symbol 64 kb + i: its centre interval (lo, freq), table metadata and offset
+    int lov[4], frv[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int sel = ti[kb] << 2;
-        lf[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lf);
+        const int lf = __builtin_amdgcn_ds_bpermute(sel, t_lf);
+        lov[kb] = lf & 0xffff;
+        frv[kb] = (int)((uint32_t)lf >> 16);
         sfb[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
         sS[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
         slm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
@@ -888,18 +890,19 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     int q0 = 0;
     uint32_t wbuf = lwin[lane];
     uint32_t wn = rdlane(wbuf, 0);
+    auto renorm_slow = [&]() {           // x < 2^31: shift in the next stream word
+        x = (x << 32) | wn;
+        ++p;
+        if (p - p0 - q0 >= 64) {
+            q0 = min(q0 + 64, RANS_WIN - 64);
+            wbuf = lwin[q0 + lane];
+        }
+        wn = rdlane(wbuf, min(p - p0 - q0, 63));
+    };
     auto renorm = [&]() {
         uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);   // 0 <=> x < RANS64_L = 2^31
         asm("" : "+s"(t));
-        if (t == 0) {
-            x = (x << 32) | wn;
-            ++p;
-            if (p - p0 - q0 >= 64) {
-                q0 = min(q0 + 64, RANS_WIN - 64);
-                wbuf = lwin[q0 + lane];
-            }
-            wn = rdlane(wbuf, min(p - p0 - q0, 63));
-        }
+        if (t == 0) renorm_slow();
         x = uni64(x);
     };
     const uint16_t* img16 = a.cdf16;
@@ -908,15 +911,34 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     for (int kb = 0; kb < 4; ++kb) {
         const int cnt_i = __builtin_amdgcn_readfirstlane(min(64, Mlat - kb * 64));
         if (cnt_i <= 0) break;
-        for (int ii = 0; ii < cnt_i; ++ii) {
-            const uint32_t cum = (uint32_t)x & 0xffffu;
-            const uint32_t lfi = rdlane((uint32_t)lf[kb], ii);
-            const uint32_t d = cum - (lfi & 0xffffu), fr = lfi >> 16;
-            if (d < fr) {                               // the most probable symbol (value 0)
-                x = (unsigned long long)fr * (x >> 16) + d;
-                renorm();
-                continue;                               // symv[kb] lane ii already holds the centre index
+        // one most-probable symbol: a compare, the 64-bit state update, a (rare) renormalisation
+        auto fast = [&](uint32_t lo, uint32_t fr) -> bool {
+            const uint32_t d = ((uint32_t)x & 0xffffu) - lo;
+            if (d >= fr) return false;
+            x = (unsigned long long)fr * (x >> 16) + d;
+            const uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);
+            if (__builtin_expect(t == 0, 0)) renorm_slow();
+            return true;
+        };
+        int ii = 0;
+        while (ii < cnt_i) {
+            // runs of most-probable symbols, 4 per iteration: the 8 interval reads (v_readlane, independent of the
+            // state) first, then 4 compare-and-update steps with forward exits, one back edge per 4 symbols
+            while (ii + 4 <= cnt_i) {
+                const uint32_t l0 = rdlane((uint32_t)lov[kb], ii), f0 = rdlane((uint32_t)frv[kb], ii);
+                const uint32_t l1 = rdlane((uint32_t)lov[kb], ii + 1), f1 = rdlane((uint32_t)frv[kb], ii + 1);
+                const uint32_t l2 = rdlane((uint32_t)lov[kb], ii + 2), f2 = rdlane((uint32_t)frv[kb], ii + 2);
+                const uint32_t l3 = rdlane((uint32_t)lov[kb], ii + 3), f3 = rdlane((uint32_t)frv[kb], ii + 3);
+                if (!fast(l0, f0)) break;
+                if (!fast(l1, f1)) { ii += 1; break; }
+                if (!fast(l2, f2)) { ii += 2; break; }
+                if (!fast(l3, f3)) { ii += 3; break; }
+                ii += 4;
             }
+            while (ii < cnt_i && fast(rdlane((uint32_t)lov[kb], ii), rdlane((uint32_t)frv[kb], ii))) ++ii;
+            if (ii >= cnt_i) break;
+            // another symbol: the two-level search of rans_row on the table image in global memory
+            const uint32_t cum = (uint32_t)x & 0xffffu;
             const int fb = rdlane_i(sfb[kb], ii), S = rdlane_i(sS[kb], ii);
             const int lm2 = rdlane_i(slm[kb], ii), ca = rdlane_i(sca[kb], ii);
             const uint32_t cv = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + ca + lane2);
@@ -946,6 +968,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                 v = (raw & 1) ? -v - 1 : v + lm2;
             }
             symv[kb] = lane == ii ? v : symv[kb];
+            ++ii;
         }
     }
     RSTAMP(2);
