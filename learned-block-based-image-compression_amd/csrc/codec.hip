@@ -72,7 +72,11 @@ struct Layer {
 // sampled per-kernel timing (lbc_profile_begin / lbc_profile_end): sampled launches stamp their span
 // into a device slot {max(~start), max(end)}; one slot range per graph, zeroed at every replay
 constexpr int kSlotsPerRange = 4096;
+#ifdef LBIC_PHASE_DIAG
+constexpr int kSlotU64 = 32;      // + per-phase max / sum / workgroup count (diagnostic build)
+#else
 constexpr int kSlotU64 = 16;      // 8 XCDs x {max(~start), max(end)}
+#endif
 constexpr int kRanges = 6;        // 0 encoder graph, 1..4 raster decoder lanes, 5 wavefront decoder graph
 struct Prof {
     int sample_every = 0;
@@ -1196,6 +1200,21 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
                 fprintf(stderr, "\n");
             }
             if (span < 0) continue;   // not executed since the last reset
+#ifdef LBIC_PHASE_DIAG
+            if (r.cls == 0 && t[31]) {
+                static double pmax[5], psum[5], nl;
+                for (int i = 1; i <= 4; ++i) { pmax[i] += (double)t[16 + i]; psum[i] += (double)t[24 + i] / (double)t[31]; }
+                nl += 1;
+                if (&r == &p.recs.back() || true) {
+                    static int printed = 0;
+                    if (++printed % 50 == 0 || &r == &p.recs.back())
+                        fprintf(stderr, "[diag k_gemm_s] launches %.0f  critical-WG cycles since start: prologue %.0f "
+                                "loads+mfma %.0f reduce %.0f epilogue %.0f | mean WG: %.0f %.0f %.0f %.0f\n", nl,
+                                pmax[1] / nl, pmax[2] / nl, pmax[3] / nl, pmax[4] / nl, psum[1] / nl, psum[2] / nl,
+                                psum[3] / nl, psum[4] / nl);
+                }
+            }
+#endif
             acc[r.cls].launches += 1;
             acc[r.cls].total_ms += (double)span * 1e-5;     // 100 MHz ticks -> ms
             acc[r.cls].flops += r.flops;

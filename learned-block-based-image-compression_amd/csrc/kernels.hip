@@ -26,6 +26,32 @@ namespace lbic {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// Kernel arguments are read with scalar loads through the scalar cache.  hipcc fetches the large argument
+// blocks field by field at first use, in several dependent rounds (a branch on one argument, then the loads
+// it guards, then a wait...), each an L2 round trip.  One asm statement touching every 64-byte line of the
+// block up front turns that into one round trip: the later, compiler-placed loads hit the scalar cache.
+// (Scalar LOADS only: nothing is written through the scalar cache.)
+template <int NLINES>
+__device__ __forceinline__ void warm_kernargs() {
+    static_assert(NLINES >= 1 && NLINES <= 10, "kernarg lines");
+    const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9;
+    if constexpr (NLINES <= 3) {
+        asm volatile("s_load_dword %0, %3, 0x0\n\ts_load_dword %1, %3, 0x40\n\ts_load_dword %2, %3, 0x80\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=s"(d0), "=s"(d1), "=s"(d2) : "s"(kp) : "memory");
+    } else {
+        asm volatile("s_load_dword %0, %10, 0x0\n\ts_load_dword %1, %10, 0x40\n\ts_load_dword %2, %10, 0x80\n\t"
+                     "s_load_dword %3, %10, 0xc0\n\ts_load_dword %4, %10, 0x100\n\ts_load_dword %5, %10, 0x140\n\t"
+                     "s_load_dword %6, %10, 0x180\n\ts_load_dword %7, %10, 0x1c0\n\ts_load_dword %8, %10, 0x200\n\t"
+                     "s_load_dword %9, %10, 0x230\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(d0), "=s"(d1), "=s"(d2), "=s"(d3), "=s"(d4), "=s"(d5), "=s"(d6), "=s"(d7), "=s"(d8), "=s"(d9)
+                     : "s"(kp) : "memory");
+    }
+}
+static_assert(sizeof(GemmArgs) <= 0x240 && sizeof(GemmArgs) > 0x230, "warm_kernargs<10> covers GemmArgs");
+static_assert(sizeof(RansArgs) <= 0xC0, "warm_kernargs<3> covers RansArgs");
+
 static int launch_status(const char* what) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, std::string(what) + " launch failed: " + hipGetErrorString(e));
@@ -63,6 +89,26 @@ __device__ unsigned long long* g_phase;
     } while (0)
 #else
 #define PHASE(i) do {} while (0)
+#endif
+
+#ifdef LBIC_PHASE_DIAG
+// diagnostic library build only (make diag -> liblbic_diag.so, LBIC_LIB_VARIANT=diag): sampled k_gemm_s launches
+// record, per phase boundary i = 1..4, the max and the sum over workgroups of (s_memtime at i - at kernel start)
+// in slot words 16 + i / 24 + i, and the workgroup count in word 31 (lbc_profile_end prints them)
+#define DPH(i)                                                                                    \
+    do {                                                                                          \
+        if (g.ts && threadIdx.x == 0) {                                                           \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
+            if ((i) == 0) dph0_ = t_;                                                             \
+            else {                                                                                \
+                atomicMax(g.ts + 16 + (i), t_ - dph0_);                                           \
+                atomicAdd(g.ts + 24 + (i), t_ - dph0_);                                           \
+                if ((i) == 4) atomicAdd(g.ts + 31, 1ull);                                         \
+            }                                                                                     \
+        }                                                                                         \
+    } while (0)
+#else
+#define DPH(i) do {} while (0)
 #endif
 
 __device__ __forceinline__ int scale_index(float s, const float* table) {
@@ -226,6 +272,7 @@ template <int BM, int BN, int NW, int CH>
 __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
     constexpr int MS = BM / 16, NS = BN / 16, SPW = KSPLIT / NW;
     extern __shared__ __attribute__((aligned(16))) float red[];
+    warm_kernargs<10>();
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: keeps the k-loop scalar
     // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin over the 8 XCDs,
@@ -414,13 +461,27 @@ __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     f4 w[LL], a[LL];
     const SBlk bk = small_blk<RASTER>(g, m0, lane, blocks);   // issued first: the A addresses wait for it
+    if constexpr (RASTER) {
+        // the block is computed, not loaded: every address is known now, so each k-block's weight and
+        // activation fragments are requested together and the MFMA chain starts as soon as the first pair lands
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
 #pragma unroll
-    for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-    SRow rw;
-    small_offsets(g, bk, lane, rw);
-    PHASE(1);
+        for (int c = 0; c < LL; ++c) {
+            const int kb = min(kb0 + c, nkb - 1);
+            w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
+            a[c] = small_a(rw, kb);
+        }
+        PHASE(1);
+    } else {
 #pragma unroll
-    for (int c = 0; c < LL; ++c) a[c] = small_a(rw, min(kb0 + c, nkb - 1));
+        for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
+        PHASE(1);
+#pragma unroll
+        for (int c = 0; c < LL; ++c) a[c] = small_a(rw, min(kb0 + c, nkb - 1));
+    }
     // keep every load above the MFMAs (the scheduler would otherwise sink each one next to its first use
     // and wait for it there: one memory round trip per k-block)
     __builtin_amdgcn_sched_barrier(0);
@@ -445,6 +506,10 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt = blockIdx.x;
     const int n0 = nt * 16, m0 = blockIdx.y * 16;
+    warm_kernargs<10>();
+    unsigned long long dph0_ = 0;
+    (void)dph0_;
+    DPH(0);
     stamp_start(g.ts);
     PHASE(0);
     // epilogue operands of this thread's output element (threads 0..255; the rest load a duplicate)
@@ -464,6 +529,7 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
         else blocks.p += (long)c * g.ctr_stride;
     }
     f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    DPH(1);
     if constexpr (L <= 12) {
         acc = small_slice<L, RASTER, EXACT>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
     } else {
@@ -471,9 +537,11 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
             acc = small_slice<11, RASTER>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
     }
     PHASE(3);
+    DPH(2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[wave * 256 + i * 64 + lane] = acc[i];
     __syncthreads();
+    DPH(3);
     PHASE(4);
     if (threadIdx.x < 256) {
         const int e = threadIdx.x;
@@ -484,6 +552,7 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
         if (row < g.M && col < g.N) epilogue(g, v, row, col, blocks, bcol, xv);
     }
     PHASE(5);
+    DPH(4);
     stamp_end(g.ts);
 }
 
@@ -565,7 +634,9 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     if (gemm_class(g) == 0) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
-        const bool raster = g.raster && g.ctr && g.need_blocks;
+        // the computed-block (RASTER) variant also serves every dense-only GEMM: its A rows need no block, and the
+        // block-list variant would make their addresses wait for a block-index load (one memory round trip)
+        const bool raster = (g.raster && g.ctr && g.need_blocks) || !g.need_blocks;
         if (g.raster && !g.ctr) return set_error(LBC_E_ARG, "raster GEMM needs the row counter");
         // every slice exactly L k-blocks: no (L+1)-th block to load (loads are what a launch waits for)
         const bool exact = ((g.K >> 4) % KSPLIT) == 0 && g_exact;
@@ -992,6 +1063,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
 
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
+    warm_kernargs<3>();
     stamp_start(a.ts);
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * RANS_WPB + (threadIdx.x >> 6);
@@ -1003,6 +1075,7 @@ __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a)
 // the wave's own loads
 __global__ __launch_bounds__(64) void k_rans_decode_sparse(const RansArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
+    warm_kernargs<3>();
     stamp_start(a.ts);
     rans_row_sparse(a, lwin, blockIdx.x, threadIdx.x);
     stamp_end(a.ts);
