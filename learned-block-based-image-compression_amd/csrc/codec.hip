@@ -290,10 +290,12 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
     std::vector<int4> dec((size_t)Hb * Wb * n_img);
     for (int s = 0; s < Hb * Wb; ++s)
         for (int img = 0; img < n_img; ++img) dec[(size_t)s * n_img + img] = make_int4(img, s / Wb, s % Wb, 0);
-    // the GEMM kernel addresses rows with 32-bit element offsets
-    if ((double)n_img * (Hb + 2) * (Wb + 4) * m->Cx >= 2147483647.0 ||
-        (double)mmax * m->P * std::max({m->C1P, m->NP, m->C2P}) * 5 >= 2147483647.0)
-        return set_error(LBC_E_ARG, "frame batch too large for 32-bit offsets; split the batch");
+    // the GEMM kernels address A rows with unsigned 32-bit float4 offsets from a segment base (kernels.hip, Rows):
+    // up to 2^34 floats (64 GB) per buffer
+    const double lim = 17179869184.0;
+    if ((double)n_img * (Hb + 2) * (Wb + 4) * m->Cx >= lim || (double)n_img * Hb * Wb * m->Cx >= lim ||
+        (double)mmax * m->P * std::max({m->C1P, m->NP, m->C2P}) * 5 >= lim)
+        return set_error(LBC_E_ARG, "frame batch too large (a workspace buffer above 64 GB); split the batch");
     int rc;
     if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4)))) return rc;
     if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4)))) return rc;

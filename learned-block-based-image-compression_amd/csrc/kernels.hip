@@ -217,13 +217,15 @@ struct Frag {
 constexpr int MAXSEG = 6;
 
 // Source addressing without branches in the k-loop: every lane precomputes, per segment t and row
-// subtile s, a 32-bit element offset from that segment's base pointer; a k-block then selects its
-// segment with uniform compares (SALU) and the offset with v_cndmask, so the compiler never branches
-// around a load (a branch per load makes hipcc drain vmcnt(0) each time: cdna_hip_programming.md §5,
-// "Three .s-level traps", (c)).
+// subtile s, a 32-bit offset from that segment's base pointer; a k-block then selects its segment with
+// uniform compares (SALU) and the offset with v_cndmask, so the compiler never branches around a load (a
+// branch per load makes hipcc drain vmcnt(0) each time: cdna_hip_programming.md §5, "Three .s-level traps",
+// (c)).  Offsets count float4s (every row offset, tap offset and k-block start is a multiple of 4 floats:
+// widths and 3B^2 are padded to 16) and are unsigned: computed in 64 bits, they address 2^32 float4s (64 GB)
+// from a base, so a ganged decoder workspace of more than 2^31 floats stays in range at no cost per load.
 template <int MS>
 struct Rows {
-    int off[MAXSEG][MS];
+    unsigned off[MAXSEG][MS];
 };
 
 template <int MS, int NS>
@@ -232,7 +234,7 @@ __device__ __forceinline__ void load_kb(const GemmArgs& g, int kb, int nb0, cons
     const int k = kb << 4;
     const float* base = g.seg[0].base;
     int k0 = g.seg[0].k0;
-    int o[MS];
+    unsigned o[MS];
 #pragma unroll
     for (int s = 0; s < MS; ++s) o[s] = R.off[0][s];
 #pragma unroll
@@ -243,9 +245,9 @@ __device__ __forceinline__ void load_kb(const GemmArgs& g, int kb, int nb0, cons
 #pragma unroll
         for (int s = 0; s < MS; ++s) o[s] = in ? R.off[t][s] : o[s];
     }
-    const int kk = k - k0 + q4;
+    const unsigned kk4 = (unsigned)(k - k0 + q4) >> 2;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) f.a[s] = *reinterpret_cast<const f4*>(base + o[s] + kk);
+    for (int s = 0; s < MS; ++s) f.a[s] = reinterpret_cast<const f4*>(base)[o[s] + kk4];
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
 #pragma unroll
     for (int j = 0; j < NS; ++j) f.w[j] = Wt[((long)kb * g.NB16 + nb0 + j) * 64];
@@ -295,13 +297,14 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         const int r = min(m0 + 16 * s + (lane & 15), g.M - 1);
         const int m = r / g.P, p = r - m * g.P;
         const int4 b = g.need_blocks ? blocks[m] : make_int4(0, 0, 0, 0);   // dense-only GEMMs skip this load
-        const int zrow = ((b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p]) * g.geo.Cx;
-        const int xrow = ((b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
+        const long zrow = (((long)b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p]) * g.geo.Cx;
+        const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
 #pragma unroll
         for (int t = 0; t < MAXSEG; ++t) {
             const Seg& sg = g.seg[t];
-            R.off[t][s] = sg.kind == SEG_DENSE ? r * sg.ld
-                        : sg.kind == SEG_ZTAP ? zrow + (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : xrow;
+            const long o = sg.kind == SEG_DENSE ? (long)r * sg.ld
+                         : sg.kind == SEG_ZTAP ? zrow + (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : xrow;
+            R.off[t][s] = (unsigned)(o >> 2);
         }
     }
 
@@ -389,7 +392,7 @@ typedef const float __attribute__((address_space(1)))* gfloat_p;   // global (no
 struct SRow {            // per-lane A addressing of every segment, computed once per launch
     gfloat_p base[MAXSEG];
     int k0[MAXSEG];
-    int off[MAXSEG];    // element offset of this lane's row in segment t, minus k0 (plus q4)
+    unsigned off[MAXSEG];   // float4 offset of this lane's row in segment t, minus k0 (plus q4), mod 2^32 (Rows)
 };
 
 // this lane's A row: the row, its block (img, v, h) when a segment or the epilogue needs it, and its
@@ -421,8 +424,8 @@ __device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, c
 
 __device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, int lane, SRow& s) {
     const int4 b = k.b;
-    const int zrow = ((b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx) * g.geo.Cx;
-    const int xrow = ((b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
+    const long zrow = (((long)b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx) * g.geo.Cx;
+    const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
     const int q4 = (lane >> 4) * 4;
 #pragma unroll
     for (int t = 0; t < MAXSEG; ++t) {
@@ -432,7 +435,8 @@ __device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, 
         // opaque from here on: the per-k-block selects pick values, not kernel-argument addresses
         // (a selected address would become one dependent scalar load per k-block)
         asm volatile("" : "+s"(s.base[t]), "+s"(s.k0[t]));
-        s.off[t] = k.r * sg.ld + sg.zs * zrow + sg.xs * xrow + sg.tap - sg.k0 + q4;
+        const long o = (long)k.r * sg.ld + (sg.zs ? zrow : 0l) + (sg.xs ? xrow : 0l) + sg.tap - sg.k0 + q4;
+        s.off[t] = (unsigned)(o >> 2);     // may wrap below zero: + k / 4 in small_a lands in range
     }
 }
 
@@ -440,14 +444,14 @@ __device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, 
 __device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
     const int k = kb << 4;
     gfloat_p base = rw.base[0];
-    int o = rw.off[0];
+    unsigned o = rw.off[0];
 #pragma unroll
     for (int t = 1; t < MAXSEG; ++t) {
         const bool in = k >= rw.k0[t];     // wave-uniform; unused segments have k0 past K
         base = in ? rw.base[t] : base;
         o = in ? rw.off[t] : o;
     }
-    return *reinterpret_cast<const f4 __attribute__((address_space(1)))*>(base + o + k);
+    return reinterpret_cast<const f4 __attribute__((address_space(1)))*>(base)[o + (unsigned)(k >> 2)];
 }
 
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks

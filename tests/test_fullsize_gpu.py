@@ -128,3 +128,28 @@ def test_config_full_size_roundtrip(name):
     blocks = [(0, 0), (0, Wb - 1), (1, 1), (Hb // 2, Wb // 3), (Hb - 1, 0), (Hb - 1, Wb - 1)]
     _teacher_forced(arch, sd, xb, r["zhat"][0].cpu().numpy(), r["symbols"][0].cpu().numpy(),
                     r["indexes"][0].cpu().numpy(), blocks)
+
+
+def test_gang_past_int32_offsets():
+    """One encode and one raster decode pass over 1160 frames of 768x768 (a gang of 36 32-frame batches, as
+    bench.py --gang): the padded reconstruction workspace holds 2.18e9 floats, past the int32 element range the
+    GEMMs' A-row offsets once had (kernels.hip Rows: unsigned float4 offsets, 64 GB per buffer).  The last
+    image -- the one furthest from the base -- must equal its own single-image encode, and decode(encode) must
+    be bit-exact over the whole gang."""
+    from lbic.arch import Arch
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    m = _model(arch, synth_state_dict(arch, 1337, rate="low"))
+    n, Hb, Wb = 1160, 96, 96
+    assert n * (Hb + 2) * (Wb + 4) * arch.cx > 2 ** 31
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randint(0, 256, (n, Hb, Wb, arch.cx), generator=gen, device="cuda", dtype=torch.uint8)
+    x = x.float().div_(255.0).sub_(0.5)
+    one = m.compress_batch(x[-1:].clone())
+    r = m.compress_batch(x)
+    del x
+    assert torch.equal(r["symbols"][-1], one["symbols"][0]) and torch.equal(r["indexes"][-1], one["indexes"][0])
+    assert torch.equal(r["zhat"][-1], one["zhat"][0])
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    del r["symbols"], r["indexes"]
+    z = m.decompress_batch(streams, Hb, Wb)
+    assert torch.equal(z, r["zhat"]), "gang decode differs from the encoder's reconstruction"
