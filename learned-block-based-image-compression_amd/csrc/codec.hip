@@ -146,6 +146,11 @@ struct lbc_model {
     // per-shape workspace
     int ws_n = 0, ws_Hb = 0, ws_Wb = 0, Mmax = 0;
     DevBuf zpad, blocks_enc, blocks_dec;
+    // layer-0 map cache of the context net (KS[1] = 3): cell (img, v, h) = LeakyReLU(layer 0) at block position
+    // (v, h), zpad geometry [n_img][Hb+2][Wb+4][C1P]; cells_enc = the cells each wavefront step computes
+    bool l0_on = false;
+    DevBuf l0, cells_enc;
+    std::vector<int> cell_off, cell_cnt;
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
@@ -296,9 +301,41 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
     if ((double)n_img * (Hb + 2) * (Wb + 4) * m->Cx >= lim || (double)n_img * Hb * Wb * m->Cx >= lim ||
         (double)mmax * m->P * std::max({m->C1P, m->NP, m->C2P}) * 5 >= lim)
         return set_error(LBC_E_ARG, "frame batch too large (a workspace buffer above 64 GB); split the batch");
+    // Layer-0 map cache (KS[1] = 3).  The context net's second layer reads layer 0 at the five positions (v-1, h-1..h+1),
+    // (v, h-1), (v, h) (a 3x3 'B' mask); the value at a position depends only on reconstructions coded
+    // before that position's own block (the 'A' taps), so it is computed once -- at its own block's step, position
+    // (0,0) -- and read from the cache afterwards, instead of at five positions in every step.  Border cells under
+    // compress() (the zero-padded window, net:342-351): row -1 is constant (k_l0_border); column -1 of row v depends
+    // on zhat(v-1, 0) and is computed at block (v, 0)'s step, column Wb of row v-1 on zhat(v-2 .. v-1, Wb-1) and is
+    // computed at block (v, Wb-1)'s step, the only step that reads it.
+    std::vector<int4> cells;
+    if (m->l0_on) {
+        m->cell_off.assign(T, 0);
+        m->cell_cnt.assign(T, 0);
+        for (int t = 0; t < T; ++t) {
+            m->cell_off[t] = (int)cells.size();
+            for (int img = 0; img < n_img; ++img)
+                for (int v = 0; v < Hb; ++v) {
+                    const int h = t - 2 * v;
+                    if (h < 0 || h >= Wb) continue;
+                    cells.push_back(make_int4(img, v, h, 0));
+                    if (h == 0) cells.push_back(make_int4(img, v, -1, 0));
+                    if (h == Wb - 1) cells.push_back(make_int4(img, v - 1, Wb, 0));
+                }
+            m->cell_cnt[t] = (int)cells.size() - m->cell_off[t];
+        }
+        if ((double)n_img * (Hb + 2) * (Wb + 4) * m->C1P >= lim)
+            return set_error(LBC_E_ARG, "frame batch too large (layer-0 cache above 64 GB); split the batch");
+    }
     int rc;
     if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4)))) return rc;
     if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4)))) return rc;
+    if (m->l0_on) {
+        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4)))) return rc;
+        const size_t b = (size_t)n_img * (Hb + 2) * (Wb + 4) * m->C1P * sizeof(float);
+        if ((rc = m->l0.alloc(b))) return rc;
+        HIPCHK(hipMemset(m->l0.p, 0, b));    // pad channels stay 0 (never written; A x 0-weight must not meet NaN)
+    }
     const size_t F = sizeof(float);
     if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
     const int gmax = n_img;      // a decoder lane may get every image (lane count is chosen per call)
@@ -531,8 +568,43 @@ int run_gdn(GemmArgs g, const Layer& L, const float* in, int ld, bool inverse, f
 // context net (get_meanscale_fast, net:389-398) for the rows of `g`; the last layer's epilogue is
 // plain (encode) or also emits the scale indexes (decode).  frame_pad: forward()'s full-frame semantics
 // (get_meanscale as nn.Sequential, net:57-65): the layer-0 map is zero outside the frame.
-int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, bool frame_pad = false) {
+// cells / ncells: the layer-0 cache cells of this wavefront step (cache mode, encoder and wavefront decoder); a
+// raster step (g.raster) computes its own block's cell plus the border cell it owns (column -1 at h = 0, column Wb
+// of the row above at h = Wb - 1).  Without either (forward(): every block at once) layer 0 runs at the five
+// positions per block as before.
+int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, bool frame_pad = false,
+            const int4* cells = nullptr, int ncells = 0) {
     int rc;
+    if (m->l0_on && (cells || g.raster)) {
+        GemmArgs c = g;
+        c.nseg = 0;
+        c.square_a = 0;
+        c.zero_oob = frame_pad;
+        c.pos_dy[0] = c.pos_dx[0] = 0;
+        if (cells) {
+            c.blocks = cells;
+            c.M = ncells;
+            c.P = 1;
+        } else {
+            int P = 1;
+            if (g.raster_h == 0) { c.pos_dy[P] = 0; c.pos_dx[P] = -1; ++P; }
+            if (g.raster_h == g.geo.Wb - 1) { c.pos_dy[P] = -1; c.pos_dx[P] = 1; ++P; }
+            c.P = P;
+            c.M = g.M * P;
+        }
+        set_layer(c, m->ctx0, EPI_LEAKY_L0, m->l0.as<float>(), m->C1P);
+        segs_ztaps(c, m->Cx);
+        if ((rc = gemm(c, s))) return rc;
+        GemmArgs d = g;
+        d.nseg = 0;
+        d.square_a = 0;
+        set_layer(d, m->ctx1, EPI_LEAKY, w.ctx1.as<float>(), m->C2P);
+        for (int t = 0; t < 5; ++t) {       // the 3x3 'B' taps of layer 1 = five cache cells, K order as packed
+            Seg& sg = d.seg[d.nseg++];
+            sg = Seg{m->l0.as<float>(), SEG_L0TAP, m->C1P, TAPS_B[t][0], TAPS_B[t][1], t * m->C1P, (t + 1) * m->C1P};
+        }
+        if ((rc = gemm(d, s))) return rc;
+    } else {
     {
         GemmArgs c = g;
         c.nseg = 0;
@@ -550,6 +622,7 @@ int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, boo
     }
     if ((rc = run_dense(g, m->ctx1, w.ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, w.ctx1.as<float>(), m->C2P, s)))
         return rc;
+    }
     if ((rc = run_dense(g, m->ctx2, w.ctx1.as<float>(), m->C2P, EPI_LEAKY, w.ctx2.as<float>(), m->C3P, s)))
         return rc;
     GemmArgs c = g;
@@ -641,6 +714,8 @@ int lbc_create(const lbc_config* cfg, lbc_model** out) {
         return set_error(LBC_E_ARG, "3*B^2 and M must be multiples of 16");
     }
     m->P = cfg->ks[1] == 3 ? 5 : 1;
+    const char* lc = getenv("LBIC_L0CACHE");       // 0: layer 0 at five positions per block (A/B runs)
+    m->l0_on = m->P == 5 && !(lc && atoi(lc) == 0);
     *out = m;
     return LBC_OK;
 }
@@ -793,7 +868,9 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
             m->prof.step(m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0);
             GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), n_img, Hb, Wb);
-            if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad);
+            if (!crc)
+                crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad,
+                              m->l0_on ? m->cells_enc.as<int4>() + m->cell_off[t] : nullptr, m->l0_on ? m->cell_cnt[t] : 0);
             if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
                                     m->bits_buf.as<float>(), m->cap);
             if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
@@ -812,6 +889,9 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     HIPCHK(hipEventRecord(m->ev[0], s));
     HIPCHK(hipMemcpyAsync(m->x_in.p, x_dev, nx * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    if (m->l0_on &&
+        (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, frame_pad ? nullptr : m->ctx0.bias.as<float>(), s)))
+        return rc;
     HIPCHK(hipGraphLaunch(m->enc_exec, s));
     m->prof.replays[0] += 1;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
@@ -994,6 +1074,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
         m->dec_key = key;
     }
     HIPCHK(hipMemsetAsync(m->ctr.p, 0, kLanes * sizeof(int), s));
+    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->ctx0.bias.as<float>(), s))) return rc;
     if (G == 1) {      // one lane: the row graphs run on the caller's stream
         for (int v = 0; v < Hb; ++v) HIPCHK(hipGraphLaunch(m->dec_exec[0], s));
         m->prof.replays[1] += Hb;
@@ -1095,7 +1176,8 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
             m->prof.step(m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0);
             const int rows = m->step_cnt[t];
             GemmArgs g = base_args(m, blocks + m->step_off[t], rows, nullptr, n_img, Hb, Wb);
-            crc = run_ctx(m, w, g, true, m->cap);
+            crc = run_ctx(m, w, g, true, m->cap, false, m->l0_on ? m->cells_enc.as<int4>() + m->cell_off[t] : nullptr,
+                          m->l0_on ? m->cell_cnt[t] : 0);
             RansArgs r = rans_args(m);
             r.idx = w.idx.as<int32_t>();
             r.ksi = w.ksi.as<float>();
@@ -1126,6 +1208,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
     }
     HIPCHK(hipEventRecord(m->ev[2], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->ctx0.bias.as<float>(), s))) return rc;
     HIPCHK(hipGraphLaunch(m->wf_exec, s));
     m->prof.replays[kRanges - 1] += 1;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;

@@ -18,16 +18,20 @@ constexpr int KSPLIT = 8;   // every GEMM output = ((s0 + s1) + ... + s7) + bias
                             // over the i-th eighth of K: identical for every tile shape, so the encoder
                             // (large wavefront M) and the decoder (M = n_img) compute bit-identical values.
 
-enum SegKind : int { SEG_DENSE = 0, SEG_ZTAP = 1, SEG_X = 2 };
-enum Epi : int { EPI_BIAS = 0, EPI_LEAKY, EPI_GDN, EPI_IGDN, EPI_QUANT, EPI_CTXIDX, EPI_CLAMPZ, EPI_SCATTER };
+// SEG_L0TAP: a cell of the context net's layer-0 map cache (KS[1] = 3; codec.hip, "layer-0 map cache"), laid
+// out like zpad ([n_img][Hb+2][Wb+4] cells) with the layer-0 width per cell
+enum SegKind : int { SEG_DENSE = 0, SEG_ZTAP = 1, SEG_X = 2, SEG_L0TAP = 3 };
+// EPI_LEAKY_L0: LeakyReLU, written to the layer-0 map cache cell of the row's (block, position) instead of row-major
+enum Epi : int { EPI_BIAS = 0, EPI_LEAKY, EPI_GDN, EPI_IGDN, EPI_QUANT, EPI_CTXIDX, EPI_CLAMPZ, EPI_SCATTER, EPI_LEAKY_L0 };
 
 struct Seg {                 // one K-range of the A operand: K columns [k0, k1)
     const float* base;       // SEG_DENSE: activations base
     int kind;
-    int ld;                  // SEG_DENSE row stride (floats)
-    int dy, dx;              // SEG_ZTAP: tap offset relative to the output position
+    int ld;                  // SEG_DENSE row stride; SEG_L0TAP cell width (floats)
+    int dy, dx;              // SEG_ZTAP / SEG_L0TAP: tap offset relative to the output position
     int k0, k1;
-    int zs, xs, tap;         // set by launch_gemm: row offset = r*ld + zs*zrow + xs*xrow + tap (no branches)
+    int zs, xs, tap;         // set by launch_gemm: row offset = r*ld + zs*cell + xs*xrow + tap (no branches), cell =
+                             // the zpad-geometry cell index of the row's position, zs = that segment's cell width
 };
 
 struct Geo {
@@ -106,5 +110,6 @@ int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s);
 int launch_copy_interior(const float* zpad, float* zout, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
 int launch_fill_interior(const float* zin, float* zpad, int n_img, int Hb, int Wb, int Cx, hipStream_t s);
+int launch_l0_border(float* l0, int n_img, int Hb, int Wb, int C, const float* bias, hipStream_t s);
 
 }  // namespace lbic

@@ -161,6 +161,22 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             g.out[(long)row * g.ldo + col] = o;
             break;
         }
+        case EPI_LEAKY_L0: {   // row = block * P + position -> the layer-0 cache cell of that position
+            const float t = v + bcol;
+            float o = t > 0.f ? t : t * 0.01f;
+            const int m = row / g.P, p = row - m * g.P;
+            int dy = 0, dx = 0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                dy = p == q ? g.pos_dy[q] : dy;
+                dx = p == q ? g.pos_dx[q] : dx;
+            }
+            const int4 b = blocks.at(m);
+            const int vv = b.y + dy, hh = b.z + dx;
+            if (g.zero_oob && (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb)) o = 0.f;
+            g.out[(((long)b.x * g.geo.Hp + vv + 2) * g.geo.Wp + hh + 2) * g.ldo + col] = o;
+            break;
+        }
         case EPI_GDN:
         case EPI_IGDN: {
             const float norm = v + bcol;
@@ -297,13 +313,12 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
         const int r = min(m0 + 16 * s + (lane & 15), g.M - 1);
         const int m = r / g.P, p = r - m * g.P;
         const int4 b = g.need_blocks ? blocks[m] : make_int4(0, 0, 0, 0);   // dense-only GEMMs skip this load
-        const long zrow = (((long)b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p]) * g.geo.Cx;
+        const long cell = ((long)b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p];
         const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
 #pragma unroll
         for (int t = 0; t < MAXSEG; ++t) {
             const Seg& sg = g.seg[t];
-            const long o = sg.kind == SEG_DENSE ? (long)r * sg.ld
-                         : sg.kind == SEG_ZTAP ? zrow + (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : xrow;
+            const long o = (long)r * sg.ld + sg.zs * cell + (sg.xs ? xrow : 0l) + sg.tap;
             R.off[t][s] = (unsigned)(o >> 2);
         }
     }
@@ -424,7 +439,7 @@ __device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, c
 
 __device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, int lane, SRow& s) {
     const int4 b = k.b;
-    const long zrow = (((long)b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx) * g.geo.Cx;
+    const long cell = ((long)b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx;
     const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
     const int q4 = (lane >> 4) * 4;
 #pragma unroll
@@ -435,7 +450,7 @@ __device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, 
         // opaque from here on: the per-k-block selects pick values, not kernel-argument addresses
         // (a selected address would become one dependent scalar load per k-block)
         asm volatile("" : "+s"(s.base[t]), "+s"(s.k0[t]));
-        const long o = (long)k.r * sg.ld + (sg.zs ? zrow : 0l) + (sg.xs ? xrow : 0l) + sg.tap - sg.k0 + q4;
+        const long o = (long)k.r * sg.ld + sg.zs * cell + (sg.xs ? xrow : 0l) + sg.tap - sg.k0 + q4;
         s.off[t] = (unsigned)(o >> 2);     // may wrap below zero: + k / 4 in small_a lands in range
     }
 }
@@ -611,7 +626,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
 
 int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     GemmArgs g = g0;
-    g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ || g.epi == EPI_SCATTER || g.zero_oob;
+    g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ || g.epi == EPI_SCATTER || g.epi == EPI_LEAKY_L0 || g.zero_oob;
     for (int t = 0; t < g.nseg && t < MAXSEG; ++t) g.need_blocks |= g.seg[t].kind != SEG_DENSE;
     if (g.M <= 0) return LBC_OK;
     if (g.K % 16 || g.K < 16) return set_error(LBC_E_ARG, "GEMM K must be a positive multiple of 16");
@@ -620,15 +635,15 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         return set_error(LBC_E_ARG, "GEMM segments must cover [0, K)");
     for (int t = 0; t < g.nseg; ++t) {
         const Seg& sg = g.seg[t];
-        if (!sg.base || (sg.k0 & 15) || (t && sg.k0 != g.seg[t - 1].k1))
+        if (!sg.base || (sg.k0 & 15) || (t && sg.k0 != g.seg[t - 1].k1) || (sg.kind == SEG_L0TAP && (sg.ld & 15)))
             return set_error(LBC_E_ARG, "bad GEMM segment");
     }
     if (!g.W || !g.bias || !g.blocks || g.P < 1 || g.P > 5) return set_error(LBC_E_ARG, "bad GEMM arguments");
     for (int t = 0; t < g.nseg; ++t) {            // branch-free row offset: r*ld + zs*zrow + xs*xrow + tap
         Seg& sg = g.seg[t];
-        sg.zs = sg.kind == SEG_ZTAP;
+        sg.zs = sg.kind == SEG_ZTAP ? g.geo.Cx : sg.kind == SEG_L0TAP ? sg.ld : 0;
         sg.xs = sg.kind == SEG_X;
-        sg.tap = sg.kind == SEG_ZTAP ? (sg.dy * g.geo.Wp + sg.dx) * g.geo.Cx : 0;
+        sg.tap = sg.zs * (sg.dy * g.geo.Wp + sg.dx);
         if (sg.kind != SEG_DENSE) sg.ld = 0;
     }
     for (int t = g.nseg; t < MAXSEG; ++t) {       // unused segments: never selected (k0 past every k)
@@ -1155,6 +1170,37 @@ __global__ void k_fill_interior(const float* __restrict__ zin, float* __restrict
         const long dst = ((long)(img * (Hb + 2) + v + 2) * (Wb + 4) + h + 2) * Cx + c;
         *reinterpret_cast<f4*>(zpad + dst) = *reinterpret_cast<const f4*>(zin + e);
     }
+}
+
+// Layer-0 map cache (KS[1] = 3, codec.hip) before a closed loop: every channel of the cells of block row -1 (columns
+// -1 .. Wb) and of columns -1 and Wb of every block row set to LeakyReLU(bias) (compress(): layer 0 of the
+// zero-padded window, net:342-351, where every tap is zero) or to 0 (bias = null: forward()'s frame padding).  The
+// GEMM computes such a cell as (slice sums of zeros) + bias -> LeakyReLU, i.e. the same value.  Columns -1 / Wb
+// of rows >= 0 hold data-dependent values under compress(): the closed loops compute them before they are read.
+__global__ void k_l0_border(float* __restrict__ l0, int n_img, int Hb, int Wb, int C, const float* __restrict__ bias) {
+    const int per_img = (Wb + 2) + 2 * Hb;            // top row, then (left, right) of each block row
+    const long total = (long)n_img * per_img * C;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const long t = i / C;
+        const int img = (int)(t / per_img), k = (int)(t % per_img);
+        int v, h;
+        if (k < Wb + 2) { v = -1; h = k - 1; }
+        else { v = (k - (Wb + 2)) >> 1; h = ((k - (Wb + 2)) & 1) ? Wb : -1; }
+        float val = 0.f;
+        if (bias) {
+            const float b = bias[c];
+            val = b > 0.f ? b : b * 0.01f;
+        }
+        l0[(((long)img * (Hb + 2) + v + 2) * (Wb + 4) + h + 2) * C + c] = val;
+    }
+}
+
+int launch_l0_border(float* l0, int n_img, int Hb, int Wb, int C, const float* bias, hipStream_t s) {
+    const long total = (long)n_img * ((Wb + 2) + 2 * Hb) * C;
+    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_l0_border, dim3(blocks), dim3(256), 0, s, l0, n_img, Hb, Wb, C, bias);
+    return launch_status("l0 border");
 }
 
 int launch_fill_interior(const float* zin, float* zpad, int n_img, int Hb, int Wb, int Cx, hipStream_t s) {

@@ -326,3 +326,36 @@ def test_gang_decode_many_rows(name, n_img):
     # and as two passes of the same handle with different row counts (graphs rebuilt per shape)
     z2 = m.decompress_batch(streams[:17], *g["x"].shape[:2])
     assert torch.equal(z2, r["zhat"][:17])
+
+
+@pytest.mark.parametrize("shape", [(8, 12), (5, 1), (1, 7), (6, 2)])
+def test_layer0_cache_equals_five_positions(shape, monkeypatch):
+    """KS[1] = 3: the context net's layer-0 map cache (codec.hip, computed once per block at its own step, border
+    columns at the steps that own them) gives bit-identical symbols, indexes, bits and reconstructions to layer 0
+    evaluated at the five positions of every block (LBIC_L0CACHE=0), for compress(), the raster and the wavefront
+    (sub-stream) decoders and the validation loop's frame padding; ragged and one-block-wide frames included."""
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    g = load_golden("loop_tiny_ks3311")
+    arch = golden_arch(g)
+    sd = synth_state_dict(arch, int(g["weight_seed"]))
+    cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
+    models = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("LBIC_L0CACHE", on)
+        m = BlockBasedImgCompLossyNetv9(cfg)
+        m.load_state_dict(sd)
+        m.update(force=True)
+        models[on] = m
+    Hb, Wb = shape
+    rng = np.random.default_rng(11)
+    xb = torch.from_numpy(np.stack([rng.random((Hb, Wb, arch.cx), dtype=np.float32) - 0.5 for _ in range(3)])).cuda()
+    r = {k: m.compress_batch(xb, want_bits=True) for k, m in models.items()}
+    for key in ("symbols", "indexes", "bits", "zhat"):
+        assert torch.equal(r["0"][key], r["1"][key]), key
+    m1 = models["1"]
+    st = m1.entropy_encode(r["1"]["symbols"], r["1"]["indexes"])
+    assert torch.equal(m1.decompress_batch(st, Hb, Wb), r["1"]["zhat"])
+    rows = m1.entropy_encode(r["1"]["symbols"], r["1"]["indexes"], fmt="rows", Hb=Hb, Wb=Wb)
+    assert torch.equal(m1.decompress_batch(rows, Hb, Wb, fmt="rows"), r["1"]["zhat"])
+    v = {k: m.validate_recu_reco(xb.permute(0, 3, 1, 2)) for k, m in models.items()}
+    assert torch.equal(v["0"][0], v["1"][0]) and torch.equal(v["0"][1], v["1"][1])
