@@ -73,10 +73,6 @@ def parse_args(argv=None):
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
     ap.add_argument("--rate", default="low", choices=("low", "high"), help="synthetic weight operating point")
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
-    ap.add_argument("--enc-cu-frac", type=float, default=1.0,
-                    help="fraction of the CUs the encoder's stream may use (CU mask; 1 = all)")
-    ap.add_argument("--dec-cu-frac", type=float, default=1.0,
-                    help="fraction of the CUs each decoder stream may use (the complement of the encoder's first)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts, unless already in the environment): "
                          "every busy stream needs a hardware queue of its own (lbic/streams.py)")
@@ -205,26 +201,7 @@ def main():
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    masks = None
-    if args.enc_cu_frac < 1.0 or args.dec_cu_frac < 1.0:
-        from lbic.streams import cu_mask
-        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        me = cu_mask(args.enc_cu_frac, ncu) if args.enc_cu_frac < 1.0 else None
-        md = None
-        if args.dec_cu_frac < 1.0:     # the decoders' share, taken from the CUs the encoder does not use first
-            full = cu_mask(1.0, ncu)
-            free = [f & ~e for f, e in zip(full, me)] if me else full
-            want = int(round(args.dec_cu_frac * ncu))
-            md = [0] * len(full)
-            have = 0
-            for pref in (free, [f & ~x for f, x in zip(full, free)]):
-                for i in range(ncu):
-                    if have < want and pref[i // 32] >> (i % 32) & 1 and not md[i // 32] >> (i % 32) & 1:
-                        md[i // 32] |= 1 << (i % 32)
-                        have += 1
-        masks = [me] + [md] * ndec
-        log(f"[bench] CU masks: encoder {me}, decoders {md}")
-    s_enc, *s_decs = dedicated_streams(1 + ndec, dev, masks)
+    s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
     enc_model = make_model()
     dec_models = [make_model() for _ in range(ndec)]
     handles = [enc_model] + dec_models
