@@ -73,6 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
     ap.add_argument("--rate", default="low", choices=("low", "high"), help="synthetic weight operating point")
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
+    ap.add_argument("--share-weights", type=int, default=1,
+                    help="1: decoder handles share the encoder handle's device weights (lbc_create_sibling)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts, unless already in the environment): "
                          "every busy stream needs a hardware queue of its own (lbic/streams.py)")
@@ -203,7 +205,8 @@ def main():
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
     s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
     enc_model = make_model()
-    dec_models = [make_model() for _ in range(ndec)]
+    # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
+    dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
     handles = [enc_model] + dec_models
     plock = threading.Lock()
 

@@ -48,6 +48,13 @@ typedef struct {
 int lbc_create(const lbc_config *cfg, lbc_model **out);
 void lbc_destroy(lbc_model *m);
 
+/* A second handle on the same finalized weights (no reference counterpart: the reference keeps one model per
+ * process and codes one image at a time).  The packed device weights are shared read-only; the new handle has
+ * its own workspaces, graphs and device entropy tables (copied from src's current ones), so it can code on
+ * another stream from another thread while src is busy.  A later lbc_finalize on either handle gives that
+ * handle a fresh weight set and leaves the other's untouched; destroy order is free. */
+int lbc_create_sibling(const lbc_model *src, lbc_model **out);
+
 /* Module.load_state_dict for one tensor under its reference state-dict name
  * (e.g. "prtr_forward3.0.gamma", "get_meanscale.6.bias").  Buffers (mask, pedestal, bound, the
  * entropy-model buffers) are accepted and ignored: masks and reparametrisation constants are

@@ -122,6 +122,12 @@ struct Work {
     DevBuf ctx0, ctx1, ctx2, ksi, e0, e1, yq, d0, d1, idx;
 };
 
+// The packed device weights of one finalized state dict: shared (read-only) by every handle made from it with
+// lbc_create_sibling, so several handles decoding side by side keep one copy in the Infinity Cache
+struct Net {
+    Layer ctx0, ctx1, ctx2, ctx3, enc0, g0, e1, g1, e2, g2, e3, dec0, ig0, d1, ig1, d2, ig2, d3;
+};
+
 static const int TAPS_A[4][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}};       // masked_conv2d.py:9-17 'A'
 static const int TAPS_B[5][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0}};  // 'B' adds the centre
 
@@ -135,7 +141,7 @@ struct lbc_model {
     int NP = 0, C1P = 0, C2P = 0, C3P = 0;   // widths padded to 16 (activation row strides)
     std::map<std::string, HostT> host;
     bool finalized = false;
-    Layer ctx0, ctx1, ctx2, ctx3, enc0, g0, e1, g1, e2, g2, e3, dec0, ig0, d1, ig1, d2, ig2, d3;
+    std::shared_ptr<Net> net = std::make_shared<Net>();
     EntropyTables tabs;
     bool tabs_set = false;
     DevBuf table_dev, cdf16_dev, tmeta_dev;
@@ -592,13 +598,13 @@ int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, boo
             c.P = P;
             c.M = g.M * P;
         }
-        set_layer(c, m->ctx0, EPI_LEAKY_L0, m->l0.as<float>(), m->C1P);
+        set_layer(c, m->net->ctx0, EPI_LEAKY_L0, m->l0.as<float>(), m->C1P);
         segs_ztaps(c, m->Cx);
         if ((rc = gemm(c, s))) return rc;
         GemmArgs d = g;
         d.nseg = 0;
         d.square_a = 0;
-        set_layer(d, m->ctx1, EPI_LEAKY, w.ctx1.as<float>(), m->C2P);
+        set_layer(d, m->net->ctx1, EPI_LEAKY, w.ctx1.as<float>(), m->C2P);
         for (int t = 0; t < 5; ++t) {       // the 3x3 'B' taps of layer 1 = five cache cells, K order as packed
             Seg& sg = d.seg[d.nseg++];
             sg = Seg{m->l0.as<float>(), SEG_L0TAP, m->C1P, TAPS_B[t][0], TAPS_B[t][1], t * m->C1P, (t + 1) * m->C1P};
@@ -616,18 +622,18 @@ int run_ctx(lbc_model* m, Work& w, GemmArgs g, bool with_idx, hipStream_t s, boo
             c.pos_dy[p] = m->P == 1 ? 0 : TAPS_B[p][0];
             c.pos_dx[p] = m->P == 1 ? 0 : TAPS_B[p][1];
         }
-        set_layer(c, m->ctx0, EPI_LEAKY, w.ctx0.as<float>(), m->C1P);
+        set_layer(c, m->net->ctx0, EPI_LEAKY, w.ctx0.as<float>(), m->C1P);
         segs_ztaps(c, m->Cx);
         if ((rc = gemm(c, s))) return rc;
     }
-    if ((rc = run_dense(g, m->ctx1, w.ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, w.ctx1.as<float>(), m->C2P, s)))
+    if ((rc = run_dense(g, m->net->ctx1, w.ctx0.as<float>(), m->P * m->C1P, EPI_LEAKY, w.ctx1.as<float>(), m->C2P, s)))
         return rc;
     }
-    if ((rc = run_dense(g, m->ctx2, w.ctx1.as<float>(), m->C2P, EPI_LEAKY, w.ctx2.as<float>(), m->C3P, s)))
+    if ((rc = run_dense(g, m->net->ctx2, w.ctx1.as<float>(), m->C2P, EPI_LEAKY, w.ctx2.as<float>(), m->C3P, s)))
         return rc;
     GemmArgs c = g;
     c.idx = w.idx.as<int32_t>();
-    return run_dense(c, m->ctx3, w.ctx2.as<float>(), m->C3P, with_idx ? EPI_CTXIDX : EPI_BIAS, w.ksi.as<float>(),
+    return run_dense(c, m->net->ctx3, w.ctx2.as<float>(), m->C3P, with_idx ? EPI_CTXIDX : EPI_BIAS, w.ksi.as<float>(),
                      m->C4, s);
 }
 
@@ -639,20 +645,20 @@ int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s, float* xhat = null
         GemmArgs c = g;
         c.nseg = 0;
         c.square_a = 0;
-        set_layer(c, m->dec0, EPI_BIAS, w.d0.as<float>(), m->NP);
+        set_layer(c, m->net->dec0, EPI_BIAS, w.d0.as<float>(), m->NP);
         segs_ztaps(c, m->Cx);
         seg_dense(c, w.yq.as<float>(), m->M, 4 * m->Cx, 4 * m->Cx + m->M);
         if ((rc = gemm(c, s))) return rc;
     }
     float *d0 = w.d0.as<float>(), *d1 = w.d1.as<float>();
     const int W = m->NP;
-    if ((rc = run_gdn(g, m->ig0, d0, W, true, d1, s))) return rc;
-    if ((rc = run_dense(g, m->d1, d1, W, EPI_BIAS, d0, W, s))) return rc;
-    if ((rc = run_gdn(g, m->ig1, d0, W, true, d1, s))) return rc;
-    if ((rc = run_dense(g, m->d2, d1, W, EPI_BIAS, d0, W, s))) return rc;
-    if ((rc = run_gdn(g, m->ig2, d0, W, true, d1, s))) return rc;
-    if (xhat) return run_dense(g, m->d3, d1, W, EPI_SCATTER, xhat, m->Cx, s);   // forward(): xhat, not clamped
-    return run_dense(g, m->d3, d1, W, EPI_CLAMPZ, nullptr, 0, s);
+    if ((rc = run_gdn(g, m->net->ig0, d0, W, true, d1, s))) return rc;
+    if ((rc = run_dense(g, m->net->d1, d1, W, EPI_BIAS, d0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->net->ig1, d0, W, true, d1, s))) return rc;
+    if ((rc = run_dense(g, m->net->d2, d1, W, EPI_BIAS, d0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->net->ig2, d0, W, true, d1, s))) return rc;
+    if (xhat) return run_dense(g, m->net->d3, d1, W, EPI_SCATTER, xhat, m->Cx, s);   // forward(): xhat, not clamped
+    return run_dense(g, m->net->d3, d1, W, EPI_CLAMPZ, nullptr, 0, s);
 }
 
 // encoder transform (forward_prtr_fast, net:379-382) + quantize epilogue
@@ -663,25 +669,25 @@ int run_enc(lbc_model* m, Work& w, GemmArgs g, int32_t* sym, int32_t* idx, float
         GemmArgs c = g;
         c.nseg = 0;
         c.square_a = 0;
-        set_layer(c, m->enc0, EPI_BIAS, e0, m->NP);
+        set_layer(c, m->net->enc0, EPI_BIAS, e0, m->NP);
         segs_ztaps(c, m->Cx);
         Seg& sx = c.seg[c.nseg++];
         sx = Seg{c.geo.x, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
         if ((rc = gemm(c, s))) return rc;
     }
     const int W = m->NP;
-    if ((rc = run_gdn(g, m->g0, e0, W, false, e1, s))) return rc;
-    if ((rc = run_dense(g, m->e1, e1, W, EPI_BIAS, e0, W, s))) return rc;
-    if ((rc = run_gdn(g, m->g1, e0, W, false, e1, s))) return rc;
-    if ((rc = run_dense(g, m->e2, e1, W, EPI_BIAS, e0, W, s))) return rc;
-    if ((rc = run_gdn(g, m->g2, e0, W, false, e1, s))) return rc;
+    if ((rc = run_gdn(g, m->net->g0, e0, W, false, e1, s))) return rc;
+    if ((rc = run_dense(g, m->net->e1, e1, W, EPI_BIAS, e0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->net->g1, e0, W, false, e1, s))) return rc;
+    if ((rc = run_dense(g, m->net->e2, e1, W, EPI_BIAS, e0, W, s))) return rc;
+    if ((rc = run_gdn(g, m->net->g2, e0, W, false, e1, s))) return rc;
     GemmArgs c = g;
     c.ksi = w.ksi.as<float>();
     c.ldk = m->C4;
     c.sym = sym;
     c.idx = idx;
     c.bits = bits;
-    return run_dense(c, m->e3, e1, W, EPI_QUANT, w.yq.as<float>(), m->M, s);
+    return run_dense(c, m->net->e3, e1, W, EPI_QUANT, w.yq.as<float>(), m->M, s);
 }
 
 }  // namespace
@@ -716,6 +722,30 @@ int lbc_create(const lbc_config* cfg, lbc_model** out) {
     m->P = cfg->ks[1] == 3 ? 5 : 1;
     const char* lc = getenv("LBIC_L0CACHE");       // 0: layer 0 at five positions per block (A/B runs)
     m->l0_on = m->P == 5 && !(lc && atoi(lc) == 0);
+    *out = m;
+    return LBC_OK;
+}
+
+int lbc_create_sibling(const lbc_model* src, lbc_model** out) {
+    if (!src || !out) return set_error(LBC_E_ARG, "null argument");
+    if (!src->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called on the source handle");
+    auto* m = new lbc_model();
+    m->cfg = src->cfg;
+    m->B = src->B; m->Cx = src->Cx; m->N = src->N; m->M = src->M; m->N7 = src->N7; m->N6 = src->N6;
+    m->C1 = src->C1; m->C2 = src->C2; m->C3 = src->C3; m->C4 = src->C4; m->P = src->P;
+    m->NP = src->NP; m->C1P = src->C1P; m->C2P = src->C2P; m->C3P = src->C3P;
+    m->l0_on = src->l0_on;
+    m->enc_lds_floor = src->enc_lds_floor;
+    m->net = src->net;                    // shared, read-only
+    m->finalized = true;
+    if (src->tabs_set) {                  // host copies; this handle uploads its own device tables on first use
+        m->tabs = src->tabs;
+        m->total16 = src->total16;
+        m->c16_host = src->c16_host;
+        m->meta_host = src->meta_host;
+        m->tabs_set = true;
+        m->tabs_dirty = true;
+    }
     *out = m;
     return LBC_OK;
 }
@@ -771,30 +801,37 @@ int lbc_set_tensor(lbc_model* m, const char* name, const float* host, const int6
 int lbc_finalize(lbc_model* m) {
     if (!m) return set_error(LBC_E_ARG, "null model");
     HIPCHK(hipSetDevice(m->cfg.device));
+    m->finalized = false;
+    m->net = std::make_shared<Net>();     // a new packed set: siblings made earlier keep theirs
+    // the captured graphs hold the old weight pointers
+    if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
+    if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
+    for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
+    m->dec_exec.clear();
     const int Cx = m->Cx, N = m->N, M = m->M;
     static const int one[1][2] = {{0, 0}};
     int rc;
     // context net: layer 0 = 4 masked taps; layer 1 = 1x1, or 3x3 'B' over the 5 layer-0 positions
-    if ((rc = pack_conv(m, m->ctx0, "get_meanscale.0", Cx, m->C1, 4, TAPS_A))) return rc;
-    if (m->P == 5) rc = pack_conv(m, m->ctx1, "get_meanscale.2", m->C1, m->C2, 5, TAPS_B);
-    else rc = pack_conv(m, m->ctx1, "get_meanscale.2", m->C1, m->C2, 1, one);
+    if ((rc = pack_conv(m, m->net->ctx0, "get_meanscale.0", Cx, m->C1, 4, TAPS_A))) return rc;
+    if (m->P == 5) rc = pack_conv(m, m->net->ctx1, "get_meanscale.2", m->C1, m->C2, 5, TAPS_B);
+    else rc = pack_conv(m, m->net->ctx1, "get_meanscale.2", m->C1, m->C2, 1, one);
     if (rc) return rc;
-    if ((rc = pack_conv(m, m->ctx2, "get_meanscale.4", m->C2, m->C3, 1, one))) return rc;
-    if ((rc = pack_conv(m, m->ctx3, "get_meanscale.6", m->C3, m->C4, 1, one))) return rc;
-    if ((rc = pack_first(m, m->enc0, "prtr_forward2", "prtr_forward1", Cx))) return rc;
-    if ((rc = pack_gdn(m, m->g0, "prtr_forward3.0", N))) return rc;
-    if ((rc = pack_conv(m, m->e1, "prtr_forward3.1", N, m->N7, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->g1, "prtr_forward3.2", m->N7))) return rc;
-    if ((rc = pack_conv(m, m->e2, "prtr_forward3.3", m->N7, m->N6, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->g2, "prtr_forward3.4", m->N6))) return rc;
-    if ((rc = pack_conv(m, m->e3, "prtr_forward3.5", m->N6, M, 1, one))) return rc;
-    if ((rc = pack_first(m, m->dec0, "prtr_inverse2", "prtr_inverse1", M))) return rc;
-    if ((rc = pack_gdn(m, m->ig0, "prtr_inverse3.0", N))) return rc;
-    if ((rc = pack_conv(m, m->d1, "prtr_inverse3.1", N, m->N7, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->ig1, "prtr_inverse3.2", m->N7))) return rc;
-    if ((rc = pack_conv(m, m->d2, "prtr_inverse3.3", m->N7, m->N6, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->ig2, "prtr_inverse3.4", m->N6))) return rc;
-    if ((rc = pack_conv(m, m->d3, "prtr_inverse3.5", m->N6, Cx, 1, one))) return rc;
+    if ((rc = pack_conv(m, m->net->ctx2, "get_meanscale.4", m->C2, m->C3, 1, one))) return rc;
+    if ((rc = pack_conv(m, m->net->ctx3, "get_meanscale.6", m->C3, m->C4, 1, one))) return rc;
+    if ((rc = pack_first(m, m->net->enc0, "prtr_forward2", "prtr_forward1", Cx))) return rc;
+    if ((rc = pack_gdn(m, m->net->g0, "prtr_forward3.0", N))) return rc;
+    if ((rc = pack_conv(m, m->net->e1, "prtr_forward3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->net->g1, "prtr_forward3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, m->net->e2, "prtr_forward3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->net->g2, "prtr_forward3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, m->net->e3, "prtr_forward3.5", m->N6, M, 1, one))) return rc;
+    if ((rc = pack_first(m, m->net->dec0, "prtr_inverse2", "prtr_inverse1", M))) return rc;
+    if ((rc = pack_gdn(m, m->net->ig0, "prtr_inverse3.0", N))) return rc;
+    if ((rc = pack_conv(m, m->net->d1, "prtr_inverse3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->net->ig1, "prtr_inverse3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, m->net->d2, "prtr_inverse3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, m->net->ig2, "prtr_inverse3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, m->net->d3, "prtr_inverse3.5", m->N6, Cx, 1, one))) return rc;
     m->finalized = true;
     return LBC_OK;
 }
@@ -890,7 +927,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     HIPCHK(hipMemcpyAsync(m->x_in.p, x_dev, nx * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
     if (m->l0_on &&
-        (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, frame_pad ? nullptr : m->ctx0.bias.as<float>(), s)))
+        (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, frame_pad ? nullptr : m->net->ctx0.bias.as<float>(), s)))
         return rc;
     HIPCHK(hipGraphLaunch(m->enc_exec, s));
     m->prof.replays[0] += 1;
@@ -1074,7 +1111,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
         m->dec_key = key;
     }
     HIPCHK(hipMemsetAsync(m->ctr.p, 0, kLanes * sizeof(int), s));
-    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->ctx0.bias.as<float>(), s))) return rc;
+    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s))) return rc;
     if (G == 1) {      // one lane: the row graphs run on the caller's stream
         for (int v = 0; v < Hb; ++v) HIPCHK(hipGraphLaunch(m->dec_exec[0], s));
         m->prof.replays[1] += Hb;
@@ -1208,7 +1245,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
     }
     HIPCHK(hipEventRecord(m->ev[2], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
-    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->ctx0.bias.as<float>(), s))) return rc;
+    if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s))) return rc;
     HIPCHK(hipGraphLaunch(m->wf_exec, s));
     m->prof.replays[kRanges - 1] += 1;
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;

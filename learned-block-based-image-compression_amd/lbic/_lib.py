@@ -32,6 +32,7 @@ _P = ctypes.c_void_p
 _SIGS = {
     "lbc_create": ([ctypes.POINTER(LbcConfig), ctypes.POINTER(_P)], ctypes.c_int),
     "lbc_destroy": ([_P], None),
+    "lbc_create_sibling": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
     "lbc_set_tensor": ([_P, ctypes.c_char_p, _P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int], ctypes.c_int),
     "lbc_finalize": ([_P], ctypes.c_int),
     "lbc_pmf_to_quantized_cdf": ([_P, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),

@@ -47,6 +47,28 @@ class BlockBasedImgCompLossyNetv9:
         self._pool = None
         self._pool_workers = 0
 
+    def sibling(self) -> "BlockBasedImgCompLossyNetv9":
+        """Another model object on the same loaded weights (lbc_create_sibling): the packed device weights are
+        shared, the workspaces, graphs and device entropy tables are its own, so it can code on another stream
+        from another thread while this one is busy (bench.py's decode passes).  Needs load_state_dict() first;
+        the CDFs are those of this object at the time of the call."""
+        if not self._params:
+            raise RuntimeError("load_state_dict() before sibling()")
+        m = BlockBasedImgCompLossyNetv9.__new__(BlockBasedImgCompLossyNetv9)
+        m.config, m.arch, m.device = self.config, self.arch, self.device
+        m.conditional_gaussian_model = self.conditional_gaussian_model
+        m._params = self._params
+        m.training = False
+        m._pool = None
+        m._pool_workers = 0
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().lbc_create_sibling(self._h, ctypes.byref(h)))
+        m._h = h
+        m._tables_uploaded = self._tables_uploaded
+        if self._tables_uploaded:
+            m._keep = self._keep
+        return m
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

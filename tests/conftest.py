@@ -30,3 +30,10 @@ def golden_arch(g):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+def assert_rel(a, ref, tol=1e-5, what="values"):
+    """north_star's fp32 bar: max |a - ref| <= tol * max |ref| (reconstructions: 1e-5 relative)."""
+    a, ref = np.asarray(a, np.float64), np.asarray(ref, np.float64)
+    d = float(np.abs(a - ref).max())
+    assert d <= tol * float(np.abs(ref).max()), f"{what} differ by {d:.3e} (bar {tol:g} x max|ref|)"
