@@ -7,15 +7,18 @@ the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-59
 compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
 rANS decode).  Every decode pass decodes exactly one 32-frame batch (32 frames in flight per pass).
 
-Schedule of the headline (`value`): a software pipeline over the `--steps` batches.  The encoder (own codec
-handle + HIP stream) compresses batch k+1 while `--depth` decoder handles (own handle + stream each, default
-3) each decode one earlier batch; host rANS runs on a helper thread.  Every busy stream gets a hardware queue of
-its own (lbic/streams.py; GPU_MAX_HW_QUEUES = --hw-queues).  The timed region holds exactly the
-`--steps` compressions and the `--steps` decompressions of the same batches, pipeline fill and drain
-included; inputs are resident in HBM when it starts.  Reported beside it: one decode pass in flight
-(`one_decode_in_flight`), no overlap at all (`serial_schedule`), the gang schedule (`gang_schedule`: one raster
-pass over several queued batches, more frames in flight, not the headline), and the opt-in sub-stream
-format (`substream_format`, not the reference bitstream).
+Schedule of the headline (`value`): `--workers` (default 4) workers, each a codec handle on the shared weights
+(lbc_create_sibling) with its own HIP stream and host thread, take the `--steps` batches in turn and compress,
+entropy code and decode each whole batch; so up to four 32-frame decode passes run side by side with the other
+workers' encodes.  Four, because dependent kernel chains overlap on at most four busy hardware queues
+(DESIGN.md §5); every stream gets a queue of its own (lbic/streams.py; GPU_MAX_HW_QUEUES = --hw-queues).
+`--workers 0` selects the encoder + `--depth` decoders pipeline instead (one encoder handle compresses batch k+1
+while the decoder handles decode earlier batches).  The timed region holds exactly the `--steps` compressions
+and the `--steps` decompressions of the same batches, fill and drain included; inputs are resident in HBM when
+it starts.  Reported beside it: one decode pass in flight (`one_decode_in_flight`), no overlap at all
+(`serial_schedule`), the gang schedule (`gang_schedule`: one raster pass over several queued batches, more
+frames in flight, not the headline), and the opt-in sub-stream format (`substream_format`, not the reference
+bitstream).
 
 Weights: the seeded synthetic set (lbic.weights) at the config's operating point (`--rate low`: about
 0.13 bpp on these frames, BASELINE.md's B8_lowrate point is 0.117 bpp); `--rate high` is the 12 bpp set.
@@ -75,6 +78,12 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
     ap.add_argument("--share-weights", type=int, default=1,
                     help="1: decoder handles share the encoder handle's device weights (lbc_create_sibling)")
+    ap.add_argument("--workers", type=int, default=4,
+                    help="headline schedule: W workers, each (own handle + stream + thread) compressing, entropy coding "
+                         "and decoding whole batches (0 = the encoder + --depth decoders pipeline)")
+    ap.add_argument("--enc-lds-floor", type=int, default=0,
+                    help="LDS bytes reserved per encoder GEMM workgroup (caps the encoder's workgroups per CU, leaving "
+                         "wave slots to the decode passes; lbc_set_option LBC_OPT_ENC_LDS_FLOOR)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts, unless already in the environment): "
                          "every busy stream needs a hardware queue of its own (lbic/streams.py)")
@@ -201,12 +210,15 @@ def main():
         return m
 
     depth = max(args.depth, 0)
-    ndec = max(depth, 2 if args.gang else 1, 1)
+    ndec = max(depth, 2 if args.gang else 1, args.workers - 1, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
     s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
+    if args.enc_lds_floor:
+        for m_ in [enc_model] + dec_models:
+            m_.set_encoder_lds_floor(args.enc_lds_floor)
     handles = [enc_model] + dec_models
     plock = threading.Lock()
 
@@ -235,32 +247,34 @@ def main():
             v = float(t.item())
         return v
 
-    def compress_side(ph, xb):
+    def compress_side(ph, xb, model=None, stream=None):
         """GPU compress on the encoder stream; symbols/indexes DMA'd into page-locked host buffers there."""
+        model, stream = model or enc_model, stream or s_enc
         t0 = time.perf_counter()
-        with torch.cuda.stream(s_enc):
-            r = enc_model.compress_batch(xb)
+        with torch.cuda.stream(stream):
+            r = model.compress_batch(xb)
             for k in ("symbols", "indexes"):
                 h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
                 h.copy_(r[k], non_blocking=True)
                 r[k] = h
-            s_enc.synchronize()
+            stream.synchronize()
         with plock:
             ph["encode"] += time.perf_counter() - t0
         return r
 
-    def entropy_side(r, fmt, ph):
+    def entropy_side(r, fmt, ph, model=None):
         t0 = time.perf_counter()
-        st = enc_model.entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
+        st = (model or enc_model).entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
         with plock:
             ph["entropy"] += time.perf_counter() - t0
         return st
 
-    def decode_side(i, st, fmt, ph):
+    def decode_side(i, st, fmt, ph, model=None, stream=None):
+        model, stream = model or dec_models[i], stream or s_decs[i]
         t0 = time.perf_counter()
-        with torch.cuda.stream(s_decs[i]):
-            z = dec_models[i].decompress_batch(st, Hb, Wb, fmt=fmt)
-            s_decs[i].synchronize()
+        with torch.cuda.stream(stream):
+            z = model.decompress_batch(st, Hb, Wb, fmt=fmt)
+            stream.synchronize()
         with plock:
             ph["decode"] += time.perf_counter() - t0
         return z
@@ -274,7 +288,7 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0):
+    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
         (or `gang` batches in one wavefront pass) while a helper thread entropy codes the previous one and
         `depth` decoder threads each decode `gang` queued batches per raster pass (their own handles and
@@ -293,7 +307,30 @@ def main():
                 done["count"] += 1
                 if done["last"] is None or k_ > done["last"][0]:
                     done["last"] = (k_, r_, st_, z_)
-        if depth == 0:
+        if workers:
+            # every worker (its own handle + stream) takes the next batch and compresses, entropy codes and decodes it
+            wk = list(zip([enc_model] + dec_models, [s_enc] + s_decs))[:workers]
+            nxt = dict(k=0)
+            nlock = threading.Lock()
+
+            def worker(wi):
+                m_, s_ = wk[wi]
+                while True:
+                    with nlock:
+                        k = nxt["k"]
+                        nxt["k"] += 1
+                    if k >= steps:
+                        return
+                    r_ = compress_side(ph, frames_of(base + k), m_, s_)
+                    st_ = entropy_side(r_, fmt, ph, m_)
+                    finish(base + k, r_, st_, decode_side(wi, st_, fmt, ph, m_, s_))
+
+            ths = [threading.Thread(target=worker, args=(i,)) for i in range(workers)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+        elif depth == 0:
             for k in range(steps):
                 r = compress_side(ph, frames_of(base + k))
                 st = entropy_side(r, fmt, ph)
@@ -374,11 +411,14 @@ def main():
     st0 = entropy_side(r0, "reference", scratch)
     for i in range(len(dec_models)):
         decode_side(i, st0, "reference", scratch)
+    if args.workers:       # every worker handle encodes too: build its encoder graph
+        for m_, s_ in list(zip(dec_models, s_decs))[:args.workers - 1]:
+            compress_side(scratch, frames_of(0), m_, s_)
     if args.warmup > 0:
-        pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup")
+        pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup", workers=args.workers)
 
     # ---- headline: the reference bitstream format, one 32-frame batch per decode pass
-    dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline")
+    dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline", workers=args.workers)
 
     side = {}
     if args.side_steps > 0 and depth != 1:
@@ -446,15 +486,21 @@ def main():
                 "(no checkpoints / Kodak offline)",
         "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
                                f"in the reference bitstream format (one raster rANS stream per image); each decode pass "
-                               f"decodes one {n}-frame batch ({n} frames in flight per pass), {depth} pass(es) in flight "
-                               "beside the encoder",
+                               f"decodes one {n}-frame batch ({n} frames in flight per pass), "
+                               + (f"up to {args.workers} passes in flight (one per worker)" if args.workers else
+                                  f"{depth} pass(es) in flight beside the encoder"),
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
                    "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
-                   "decode_passes_in_flight": depth, "frames_per_encode_pass": n,
-                   "schedule": "serial: encode, entropy, decode per batch" if depth == 0 else
-                   f"pipeline: encoder (own handle + stream) compresses batch k+1 while {depth} decoder handle(s) "
-                   "(own handle + stream each) decode earlier batches, host rANS on a helper thread; the timed "
-                   "region holds the compress and decompress of the same batches, fill and drain included"},
+                   "decode_passes_in_flight": args.workers or depth, "frames_per_encode_pass": n,
+                   "schedule": (f"workers: {args.workers} codec handles on one weight set, each with its own HIP stream "
+                                "and host thread, take the batches in turn and compress, entropy code (host rANS) and "
+                                "decode each whole batch" if args.workers else
+                                "serial: encode, entropy, decode per batch" if depth == 0 else
+                                f"pipeline: encoder (own handle + stream) compresses batch k+1 while {depth} decoder "
+                                "handle(s) (own handle + stream each) decode earlier batches, host rANS on a helper "
+                                "thread")
+                   + "; the timed region holds the compress and decompress of the same batches, fill and drain "
+                     "included"},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"rate_point": args.rate, "bpp": round(bpp, 5), "psnr_db": round(psnr, 3),
                     "enc_dec_bit_exact": bit_exact, "vs_ref": vs_ref},
