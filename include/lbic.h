@@ -142,6 +142,19 @@ int lbc_rans_encode_rows(const lbc_model *m, const int32_t *sym, const int32_t *
 int lbc_decode_rows(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                     float *zhat_dev, void *stream);
 
+/* Band pipeline for frames split over GPUs by block rows (no reference counterpart: the reference
+ * codes one image on one device).  compress() of block rows [v0, v0 + Hb_band) of n_img frames, x_dev
+ * [n_img][Hb_band][Wb][3B^2].  The frames' anti-diagonal wavefront codes block (v, h) at global step t = h + 2v;
+ * lbc_band_run runs this band's share of global steps [t0, t1).  halo_dev (nullable, [n_img][2][Wb][3B^2]) holds the
+ * two block rows above the band (v0-2, v0-1) as the band above last returned them in its edge_dev; it must contain
+ * every block that band coded before step t1 - 1 (so: the band above ran [t0, t1) first).  edge_dev (nullable,
+ * same shape) receives this band's last two block rows after the range.  lbc_band_end writes zhat, symbols and
+ * indexes of the band (layout as lbc_encode for Hb_band rows); the bands' symbols concatenated in row order are the
+ * frame's.  Results are bit-identical to lbc_encode on the whole frame (compress() semantics). */
+int lbc_band_begin(lbc_model *m, const float *x_dev, int n_img, int Hb_band, int Wb, int v0, void *stream);
+int lbc_band_run(lbc_model *m, int t0, int t1, const float *halo_dev, float *edge_dev, void *stream);
+int lbc_band_end(lbc_model *m, float *zhat_dev, int32_t *sym_dev, int32_t *idx_dev, float *bits_dev, void *stream);
+
 void lbc_free(void *p);
 const char *lbc_last_error(void);
 

@@ -173,6 +173,11 @@ struct lbc_model {
     std::vector<long long> enc_key, dec_key, wf_key;
     DevBuf x_in, sym_buf, idx_buf, bits_buf, ctr;
     hipStream_t cap = nullptr;
+    // band pipeline (lbc_band_*): this handle codes block rows [band_v0, band_v0 + ws_Hb) of taller frames;
+    // one captured graph per range of global wavefront steps
+    int band_v0 = -1;
+    std::map<std::pair<int, int>, hipGraphExec_t> band_exec;
+    std::vector<long long> band_key;
 };
 
 namespace {
@@ -773,6 +778,7 @@ void lbc_destroy(lbc_model* m) {
     if (m->enc_exec) (void)hipGraphExecDestroy(m->enc_exec);
     if (m->wf_exec) (void)hipGraphExecDestroy(m->wf_exec);
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
+    for (auto& kv : m->band_exec) (void)hipGraphExecDestroy(kv.second);
     if (m->cap) (void)hipStreamDestroy(m->cap);
     delete m;
 }
@@ -808,6 +814,9 @@ int lbc_finalize(lbc_model* m) {
     if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
     m->dec_exec.clear();
+    for (auto& kv : m->band_exec) (void)hipGraphExecDestroy(kv.second);
+    m->band_exec.clear();
+    m->band_key.clear();
     const int Cx = m->Cx, N = m->N, M = m->M;
     static const int one[1][2] = {{0, 0}};
     int rc;
@@ -937,6 +946,104 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     if (bits_dev) HIPCHK(hipMemcpyAsync(bits_dev, m->bits_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(m->ev[1], s));
     m->enc_timed = true;
+    return LBC_OK;
+}
+
+// ---------------------------------------------------------------- band pipeline for frames split over GPUs
+// Block rows [v0, v0 + Hb_band) of n_img frames.  The workspace is the band's: zpad rows 0..1 (the zero border of a
+// whole frame) hold the two block rows above the band, which the caller hands over before every step range.
+int lbc_band_begin(lbc_model* m, const float* x_dev, int n_img, int Hb_band, int Wb, int v0, void* stream) {
+    if (!m || !x_dev) return set_error(LBC_E_ARG, "null argument");
+    if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+    if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+    if (n_img <= 0 || Hb_band <= 0 || Wb <= 0 || v0 < 0) return set_error(LBC_E_ARG, "empty band");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = prepare_device(m))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb_band, Wb))) return rc;
+    const size_t nx = (size_t)n_img * Hb_band * Wb * m->Cx, nsym = (size_t)n_img * Hb_band * Wb * m->M;
+    if ((rc = m->x_in.alloc(nx * 4)) || (rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4)) ||
+        (rc = m->bits_buf.alloc(nsym * 4)))
+        return rc;
+    // the step-range graphs hold workspace pointers: rebuilt when any of them (or the band) changed
+    const std::vector<long long> key = {n_img, Hb_band, Wb, v0, (long long)m->x_in.p, (long long)m->zpad.p,
+                                        (long long)m->sym_buf.p, (long long)m->lane[0].ctx0.p,
+                                        (long long)m->table_dev.p, (long long)m->net.get()};
+    if (key != m->band_key) {
+        m->band_key = key;
+        for (auto& kv : m->band_exec) (void)hipGraphExecDestroy(kv.second);
+        m->band_exec.clear();
+    }
+    m->band_v0 = v0;
+    HIPCHK(hipMemcpyAsync(m->x_in.p, x_dev, nx * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb_band + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    return LBC_OK;
+}
+
+// two block rows [n_img][2][Wb][Cx] <-> zpad rows r0, r0 + 1 (interior columns)
+static int band_rows_copy(lbc_model* m, float* rows, int r0, bool to_zpad, hipStream_t s) {
+    const size_t w = (size_t)m->ws_Wb * m->Cx * sizeof(float), pitch = (size_t)(m->ws_Wb + 4) * m->Cx * sizeof(float);
+    for (int i = 0; i < m->ws_n; ++i) {
+        float* z = m->zpad.as<float>() + (((size_t)i * (m->ws_Hb + 2) + r0) * (m->ws_Wb + 4) + 2) * m->Cx;
+        float* h = rows + (size_t)i * 2 * m->ws_Wb * m->Cx;
+        HIPCHK(to_zpad ? hipMemcpy2DAsync(z, pitch, h, w, w, 2, hipMemcpyDeviceToDevice, s)
+                       : hipMemcpy2DAsync(h, w, z, pitch, w, 2, hipMemcpyDeviceToDevice, s));
+    }
+    return LBC_OK;
+}
+
+int lbc_band_run(lbc_model* m, int t0, int t1, const float* halo_dev, float* edge_dev, void* stream) {
+    if (!m || m->band_v0 < 0) return set_error(LBC_E_STATE, "lbc_band_begin() not called");
+    if (t1 < t0) return set_error(LBC_E_ARG, "bad step range");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if (halo_dev && (rc = band_rows_copy(m, const_cast<float*>(halo_dev), 0, true, s))) return rc;
+    // global step t codes block (v, h) with h + 2 v = t: the band's local step t - 2 v0
+    const int T = (int)m->step_off.size();
+    const int a = std::max(0, t0 - 2 * m->band_v0), b = std::min(T, t1 - 2 * m->band_v0);
+    if (a < b) {
+        auto it = m->band_exec.find({a, b});
+        if (it == m->band_exec.end()) {
+            std::lock_guard<std::mutex> lk(g_capture_mu);
+            HIPCHK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
+            int crc = LBC_OK;
+            const int4* blocks = m->blocks_enc.as<int4>();
+            for (int t = a; t < b && !crc; ++t) {
+                GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), m->ws_n,
+                                       m->ws_Hb, m->ws_Wb);
+                // layer 0 at five positions (no layer-0 cache): the band's row -1 is real data, not the frame border
+                crc = run_ctx(m, m->lane[0], g, false, m->cap);
+                if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
+                                        m->bits_buf.as<float>(), m->cap);
+                if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
+            }
+            hipGraph_t graph = nullptr;
+            const hipError_t e = hipStreamEndCapture(m->cap, &graph);
+            if (crc) { if (graph) (void)hipGraphDestroy(graph); return crc; }
+            if (e != hipSuccess) return set_error(LBC_E_HIP, std::string("band capture: ") + hipGetErrorString(e));
+            hipGraphExec_t ex = nullptr;
+            const hipError_t ei = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            if (ei != hipSuccess) return set_error(LBC_E_HIP, std::string("band instantiate: ") + hipGetErrorString(ei));
+            it = m->band_exec.emplace(std::make_pair(a, b), ex).first;
+        }
+        HIPCHK(hipGraphLaunch(it->second, s));
+    }
+    if (edge_dev && (rc = band_rows_copy(m, edge_dev, m->ws_Hb, false, s))) return rc;
+    return LBC_OK;
+}
+
+int lbc_band_end(lbc_model* m, float* zhat_dev, int32_t* sym_dev, int32_t* idx_dev, float* bits_dev, void* stream) {
+    if (!m || m->band_v0 < 0) return set_error(LBC_E_STATE, "lbc_band_begin() not called");
+    if (!zhat_dev || !sym_dev || !idx_dev) return set_error(LBC_E_ARG, "null argument");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, m->ws_n, m->ws_Hb, m->ws_Wb, m->Cx, s))) return rc;
+    const size_t nsym = (size_t)m->ws_n * m->ws_Hb * m->ws_Wb * m->M;
+    HIPCHK(hipMemcpyAsync(sym_dev, m->sym_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(idx_dev, m->idx_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
+    if (bits_dev) HIPCHK(hipMemcpyAsync(bits_dev, m->bits_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
+    m->band_v0 = -1;
     return LBC_OK;
 }
 

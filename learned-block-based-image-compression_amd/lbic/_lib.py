@@ -53,6 +53,9 @@ _SIGS = {
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "lbc_decode_rows": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                          ctypes.c_int, _P, _P], ctypes.c_int),
+    "lbc_band_begin": ([_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
+    "lbc_band_run": ([_P, ctypes.c_int, ctypes.c_int, _P, _P, _P], ctypes.c_int),
+    "lbc_band_end": ([_P, _P, _P, _P, _P, _P], ctypes.c_int),
     "lbc_free": ([_P], None),
     "lbc_last_error": ([], ctypes.c_char_p),
     "lbc_last_timing": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),

@@ -73,3 +73,15 @@ def test_shard_and_gather_gloo_world2():
         got = sorted(int(r[0]) for r in allrec)
         assert got == list(range(7))
         assert all(r[1] == r[0] * 10 for r in allrec)
+
+
+def test_band_rows_cover_the_frame():
+    from lbic.band import band_rows, wavefront_steps
+    for Hb in (1, 5, 6, 96, 128):
+        for P in range(1, min(Hb, 8) + 1):
+            b = band_rows(Hb, P)
+            assert [v for v, _ in b] == list(np.cumsum([0] + [r for _, r in b])[:-1])
+            assert sum(r for _, r in b) == Hb and max(r for _, r in b) - min(r for _, r in b) <= 1
+    assert wavefront_steps(96, 96) == 286
+    with pytest.raises(ValueError):
+        band_rows(3, 4)
