@@ -395,101 +395,6 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
     stamp_end(g.ts);
 }
 
-// Whole-K tiles (encoder experiments, LBIC_ENC_CFG >= 4): each wave owns a (16 WM) x (16 WN) output subtile and walks
-// all of K in k order; the KSPLIT slices are separate MFMA chains (the accumulator restarts at every slice boundary)
-// folded into a running total in slice order, ((s0 + s1) + s2) + ..., exactly the per-element arithmetic of k_gemm /
-// k_gemm_s, so no LDS reduction is needed and each lane writes its own outputs.  WN <= 2: a wave's columns stay
-// inside the packed weights' whole 32-column tiles.
-template <int WM, int WN, int NWM, int NWN, int CH>
-__global__ __launch_bounds__(NWM * NWN * 64) void k_gemm_w(const GemmArgs g) {
-    static_assert(WN <= 2, "k_gemm_w: at most 32 columns per wave");
-    warm_kernargs<10>();
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave % NWM, wn = wave / NWM;
-    const int m0 = blockIdx.y * (16 * WM * NWM) + wm * 16 * WM;
-    const int n0 = blockIdx.x * (16 * WN * NWN) + wn * 16 * WN;
-    const int q4 = (lane >> 4) * 4;
-    stamp_start(g.ts);
-    const int4* blocks = g.ctr ? g.blocks + (long)(*g.ctr) * g.ctr_stride : g.blocks;
-    if (m0 < g.M && n0 < g.N) {
-        Rows<WM> R;
-#pragma unroll
-        for (int s = 0; s < WM; ++s) {
-            const int r = min(m0 + 16 * s + (lane & 15), g.M - 1);
-            const int m = r / g.P, p = r - m * g.P;
-            const int4 b = g.need_blocks ? blocks[m] : make_int4(0, 0, 0, 0);
-            const long cell = ((long)b.x * g.geo.Hp + b.y + 2 + g.pos_dy[p]) * g.geo.Wp + b.z + 2 + g.pos_dx[p];
-            const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
-#pragma unroll
-            for (int t = 0; t < MAXSEG; ++t) {
-                const Seg& sg = g.seg[t];
-                const long o = (long)r * sg.ld + sg.zs * cell + (sg.xs ? xrow : 0l) + sg.tap;
-                R.off[t][s] = (unsigned)(o >> 2);
-            }
-        }
-        f4 acc[WM][WN], tot[WM][WN];
-#pragma unroll
-        for (int s = 0; s < WM; ++s)
-#pragma unroll
-            for (int j = 0; j < WN; ++j) acc[s][j] = tot[s][j] = f4{0.f, 0.f, 0.f, 0.f};
-        const int nkb = g.K >> 4, nb0 = n0 >> 4;
-        int sl = 0;                    // slices folded so far
-        auto fold_to = [&](int kb_next) {   // fold every slice ending at or before k-block kb_next
-            while (sl < KSPLIT && (sl + 1) * nkb / KSPLIT <= kb_next) {
-#pragma unroll
-                for (int s = 0; s < WM; ++s)
-#pragma unroll
-                    for (int j = 0; j < WN; ++j) {
-                        tot[s][j] = sl == 0 ? acc[s][j] : tot[s][j] + acc[s][j];
-                        acc[s][j] = f4{0.f, 0.f, 0.f, 0.f};
-                    }
-                ++sl;
-            }
-        };
-        fold_to(0);
-        Frag<WM, WN> fa[CH], fb[CH];
-        auto load_chunk = [&](int base, Frag<WM, WN>(&f)[CH]) {
-#pragma unroll
-            for (int c = 0; c < CH; ++c) load_kb<WM, WN>(g, min(base + c, nkb - 1), nb0, R, q4, lane, f[c]);
-        };
-        auto mma_chunk = [&](int base, Frag<WM, WN>(&f)[CH]) {
-#pragma unroll
-            for (int c = 0; c < CH; ++c)
-                if (base + c < nkb) {
-                    mma_kb<WM, WN>(g, f[c], acc);
-                    fold_to(base + c + 1);
-                }
-        };
-        int kb = 0;
-        load_chunk(kb, fa);
-        while (kb < nkb) {
-            if (kb + CH < nkb) load_chunk(kb + CH, fb);
-            mma_chunk(kb, fa);
-            kb += CH;
-            if (kb >= nkb) break;
-            if (kb + CH < nkb) load_chunk(kb + CH, fa);
-            mma_chunk(kb, fb);
-            kb += CH;
-        }
-        const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-#pragma unroll
-        for (int s = 0; s < WM; ++s)
-#pragma unroll
-            for (int j = 0; j < WN; ++j) {
-                const int col = n0 + 16 * j + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m0 + 16 * s + (lane >> 4) * 4 + r;
-                    if (row < g.M && col < g.N)
-                        epilogue(g, tot[s][j][r], row, col, BlkSrc{blocks, 0, 0, 0, 0}, g.bias[col],
-                                 gdn ? g.gx[(long)row * g.ldx + col] : 0.f);
-                }
-            }
-    }
-    stamp_end(g.ts);
-}
-
 // Small-M GEMM (the decoder's per-step batch, M = n_img rows, and the wavefront's ramp steps): one
 // 16 x 16 output tile per workgroup, 8 waves = the 8 K slices, one slice per wave.  Latency-shaped:
 // every weight and activation fragment of a slice is requested before the first MFMA (the weights
@@ -743,14 +648,6 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     return launch_status("k_gemm");
 }
 
-template <int WM, int WN, int NWM, int NWN, int CH>
-static int launch_w(const GemmArgs& g, hipStream_t s) {
-    constexpr int BM = 16 * WM * NWM, BN = 16 * WN * NWN;
-    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm_w<WM, WN, NWM, NWN, CH>), grid, dim3(NWM * NWN * 64), 0, s, g);
-    return launch_status("k_gemm_w");
-}
-
 int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     GemmArgs g = g0;
     g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ || g.epi == EPI_SCATTER || g.epi == EPI_LEAKY_L0 || g.zero_oob;
@@ -826,11 +723,6 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     // two K slices) takes 77 us per launch against 122 us for 8 waves: encode phase 100 vs 150 ms per batch.
     // LBIC_ENC_CFG selects the other shapes for A/B runs (results are identical for every shape).
     switch (g_enc_cfg) {
-        case 4: return launch_w<2, 2, 2, 2, 2>(g, s);
-        case 5: return launch_w<2, 1, 2, 2, 2>(g, s);
-        case 6: return launch_w<2, 2, 2, 2, 4>(g, s);
-        case 7: return launch_w<1, 2, 2, 2, 2>(g, s);
-        case 8: return launch_w<2, 2, 1, 1, 2>(g, s);
         case 1: return launch_cfg<64, 32, 4, 2>(g, s);
         case 2: return launch_cfg<16, 32, 8, 2>(g, s);
         case 3: return launch_cfg<32, 32, 8, 2>(g, s);
