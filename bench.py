@@ -10,8 +10,9 @@ rANS decode).  Every decode pass decodes exactly one 32-frame batch (32 frames i
 Schedule of the headline (`value`): `--workers` (default 4) workers, each a codec handle on the shared weights
 (lbc_create_sibling) with its own HIP stream and host thread, take the `--steps` batches in turn and compress,
 entropy code and decode each whole batch; so up to four 32-frame decode passes run side by side with the other
-workers' encodes.  Four, because dependent kernel chains overlap on at most four busy hardware queues
-(DESIGN.md §5); every stream gets a queue of its own (lbic/streams.py; GPU_MAX_HW_QUEUES = --hw-queues).
+workers' encodes, and a worker's host rANS of batch k overlaps its stream's compress of its next batch.  Four,
+because dependent kernel chains overlap on at most four busy hardware queues; every stream gets a
+queue of its own (lbic/streams.py; GPU_MAX_HW_QUEUES = --hw-queues).
 `--workers 0` selects the encoder + `--depth` decoders pipeline instead (one encoder handle compresses batch k+1
 while the decoder handles decode earlier batches).  The timed region holds exactly the `--steps` compressions
 and the `--steps` decompressions of the same batches, fill and drain included; inputs are resident in HBM when
@@ -313,17 +314,29 @@ def main():
             nxt = dict(k=0)
             nlock = threading.Lock()
 
+            from concurrent.futures import ThreadPoolExecutor
+
             def worker(wi):
+                # the host rANS of batch k runs on a helper thread while this worker's stream compresses its next
+                # batch, so the stream does not idle through it; then batch k is decoded
                 m_, s_ = wk[wi]
-                while True:
-                    with nlock:
-                        k = nxt["k"]
-                        nxt["k"] += 1
-                    if k >= steps:
-                        return
-                    r_ = compress_side(ph, frames_of(base + k), m_, s_)
-                    st_ = entropy_side(r_, fmt, ph, m_)
-                    finish(base + k, r_, st_, decode_side(wi, st_, fmt, ph, m_, s_))
+                prev = None                   # (k, record, future of its streams)
+                with ThreadPoolExecutor(max_workers=1) as ex:
+                    while True:
+                        with nlock:
+                            k = nxt["k"]
+                            nxt["k"] += 1
+                        cur = None
+                        if k < steps:
+                            r_ = compress_side(ph, frames_of(base + k), m_, s_)
+                            cur = (k, r_, ex.submit(entropy_side, r_, fmt, ph, m_))
+                        if prev is not None:
+                            k_, r_, f_ = prev
+                            st_ = f_.result()
+                            finish(base + k_, r_, st_, decode_side(wi, st_, fmt, ph, m_, s_))
+                        if cur is None:
+                            return
+                        prev = cur
 
             ths = [threading.Thread(target=worker, args=(i,)) for i in range(workers)]
             for th in ths:
