@@ -472,42 +472,34 @@ __device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
 // differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
 // selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
-// MS row subtiles of 16 (rows m0 + 16 s) share each weight fragment: MS independent MFMA chains per wave.
-template <int L, bool RASTER, bool EXACT, int MS>
-__device__ __forceinline__ void small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const BlkSrc& blocks,
-                                            f4 (&acc)[MS]) {
+template <int L, bool RASTER, bool EXACT = false>
+__device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const BlkSrc& blocks,
+                                          f4 acc) {
     constexpr int LL = EXACT ? L : L + 1;     // EXACT: every slice has exactly L k-blocks (K/16 divisible by 8)
     const int nkb = g.K >> 4;
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-    f4 w[LL], a[MS][LL];
-    SBlk bk[MS];
-#pragma unroll
-    for (int s = 0; s < MS; ++s) bk[s] = small_blk<RASTER>(g, m0 + 16 * s, lane, blocks);   // issued first
+    f4 w[LL], a[LL];
+    const SBlk bk = small_blk<RASTER>(g, m0, lane, blocks);   // issued first: the A addresses wait for it
     if constexpr (RASTER) {
         // the block is computed, not loaded: every address is known now, so each k-block's weight and
         // activation fragments are requested together and the MFMA chain starts as soon as the first pair lands
-        SRow rw[MS];
-#pragma unroll
-        for (int s = 0; s < MS; ++s) small_offsets(g, bk[s], lane, rw[s]);
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
 #pragma unroll
         for (int c = 0; c < LL; ++c) {
             const int kb = min(kb0 + c, nkb - 1);
             w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
-#pragma unroll
-            for (int s = 0; s < MS; ++s) a[s][c] = small_a(rw[s], kb);
+            a[c] = small_a(rw, kb);
         }
         PHASE(1);
     } else {
 #pragma unroll
         for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-        SRow rw[MS];
-#pragma unroll
-        for (int s = 0; s < MS; ++s) small_offsets(g, bk[s], lane, rw[s]);
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
         PHASE(1);
 #pragma unroll
-        for (int c = 0; c < LL; ++c)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) a[s][c] = small_a(rw[s], min(kb0 + c, nkb - 1));
+        for (int c = 0; c < LL; ++c) a[c] = small_a(rw, min(kb0 + c, nkb - 1));
     }
     // keep every load above the MFMAs (the scheduler would otherwise sink each one next to its first use
     // and wait for it there: one memory round trip per k-block)
@@ -515,39 +507,33 @@ __device__ __forceinline__ void small_slice(const GemmArgs& g, int kb0, int n, i
     PHASE(2);
 #pragma unroll
     for (int c = 0; c < LL; ++c) {
+        f4 av = a[c];
+        if (g.square_a) av = av * av;
+        f4 t = acc;
 #pragma unroll
-        for (int s = 0; s < MS; ++s) {
-            f4 av = a[s][c];
-            if (g.square_a) av = av * av;
-            f4 t = acc[s];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-            acc[s] = c < n ? t : acc[s];
-        }
+        for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+        acc = c < n ? t : acc;
     }
+    return acc;
 }
 
-// L = (K/16) / 8 k-blocks per slice (each slice L or L+1); L > 12: chunks of 12.  MS = 16-row subtiles per
-// workgroup (MS = 2: a 32 x 16 tile, each weight fragment loaded once for both subtiles).
-template <int L, bool RASTER, bool EXACT, int MS>
+// L = (K/16) / 8 k-blocks per slice (each slice L or L+1); L > 12: chunks of 12
+template <int L, bool RASTER, bool EXACT>
 __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
-    static_assert(MS == 1 || MS == 2, "k_gemm_s row subtiles");
-    __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256 * MS];
+    __shared__ __attribute__((aligned(16))) float red[KSPLIT * 256];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt = blockIdx.x;
-    const int n0 = nt * 16, m0 = blockIdx.y * 16 * MS;
+    const int n0 = nt * 16, m0 = blockIdx.y * 16;
     warm_kernargs<10>();
     unsigned long long dph0_ = 0;
     (void)dph0_;
     DPH(0);
     stamp_start(g.ts);
     PHASE(0);
-    // epilogue operands of this thread's output element (threads 0 .. 256 MS - 1; the rest load a duplicate):
-    // subtile es, element e of it
-    const int es = MS == 2 ? (threadIdx.x >> 8) : 0;
+    // epilogue operands of this thread's output element (threads 0..255; the rest load a duplicate)
     const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
-    const int erow = min(m0 + 16 * es + (el >> 4) * 4 + er, g.M - 1), ecol = min(n0 + (el & 15), g.N - 1);
+    const int erow = min(m0 + (el >> 4) * 4 + er, g.M - 1), ecol = min(n0 + (el & 15), g.N - 1);
     const float bcol = g.bias[ecol];
     const float xv = (g.epi == EPI_GDN || g.epi == EPI_IGDN) ? g.gx[(long)erow * g.ldx + ecol] : 0.f;
 
@@ -561,31 +547,27 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
         if constexpr (RASTER) blocks.v = c;
         else blocks.p += (long)c * g.ctr_stride;
     }
-    f4 acc[MS];
-#pragma unroll
-    for (int s = 0; s < MS; ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
     DPH(1);
     if constexpr (L <= 12) {
-        small_slice<L, RASTER, EXACT, MS>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
+        acc = small_slice<L, RASTER, EXACT>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
     } else {
         for (int c0 = kb0; c0 < kb1; c0 += 12)
-            small_slice<11, RASTER, false, MS>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
+            acc = small_slice<11, RASTER>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
     }
     PHASE(3);
     DPH(2);
 #pragma unroll
-    for (int s = 0; s < MS; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[(s * KSPLIT + wave) * 256 + i * 64 + lane] = acc[s][i];
+    for (int i = 0; i < 4; ++i) red[wave * 256 + i * 64 + lane] = acc[i];
     __syncthreads();
     DPH(3);
     PHASE(4);
-    if (threadIdx.x < 256 * MS) {
-        const int e = threadIdx.x & 255;
-        float v = red[es * KSPLIT * 256 + e];
+    if (threadIdx.x < 256) {
+        const int e = threadIdx.x;
+        float v = red[e];
 #pragma unroll
-        for (int i = 1; i < KSPLIT; ++i) v += red[(es * KSPLIT + i) * 256 + e];
-        const int row = m0 + 16 * es + (el >> 4) * 4 + er, col = n0 + (el & 15);
+        for (int i = 1; i < KSPLIT; ++i) v += red[i * 256 + e];
+        const int row = m0 + (el >> 4) * 4 + er, col = n0 + (el & 15);
         if (row < g.M && col < g.N) epilogue(g, v, row, col, blocks, bcol, xv);
     }
     PHASE(5);
@@ -620,11 +602,6 @@ static const int g_dec_small_max = dec_small_max();
 int gemm_class(const GemmArgs& g) {
     return (g.M <= g_small_max || (g.raster && g.M <= g_dec_small_max)) ? 0 : 1;
 }
-static int small_ms() {   // LBIC_SMALL_MS=2: 32 x 16 tiles in the small-M kernel (A/B runs)
-    const char* e = getenv("LBIC_SMALL_MS");
-    return e ? atoi(e) : 1;
-}
-static const int g_small_ms = small_ms();
 static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B experiments)
     const char* e = getenv("LBIC_EXACT");
     return e ? atoi(e) : 1;
@@ -676,9 +653,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     }
     if (gemm_class(g) == 0) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
-        // 32-row tiles (MS = 2) when LBIC_SMALL_MS=2 and the launch has more than 16 rows
-        const int ms = (g_small_ms == 2 && g.M > 16) ? 2 : 1;
-        dim3 grid((g.N + 15) / 16, (g.M + 16 * ms - 1) / (16 * ms));
+        dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
         // the computed-block (RASTER) variant also serves every dense-only GEMM: its A rows need no block, and the
         // block-list variant would make their addresses wait for a block-index load (one memory round trip)
         const bool raster = (g.raster && g.ctr && g.need_blocks) || !g.need_blocks;
@@ -687,11 +662,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         const bool exact = ((g.K >> 4) % KSPLIT) == 0 && g_exact;
         const int sel = (raster ? 1 : 0) + (exact ? 2 : 0);
         switch ((g.K >> 4) / KSPLIT) {
-#define LBIC_V(L, R, E)                                                                            \
-    do {                                                                                           \
-        if (ms == 2) hipLaunchKernelGGL((k_gemm_s<L, R, E, 2>), grid, dim3(512), 0, s, g);         \
-        else hipLaunchKernelGGL((k_gemm_s<L, R, E, 1>), grid, dim3(512), 0, s, g);                 \
-    } while (0)
+#define LBIC_V(L, R, E) hipLaunchKernelGGL((k_gemm_s<L, R, E>), grid, dim3(512), 0, s, g)
 #define LBIC_L(L)                                                                                  \
     case L:                                                                                        \
         switch (sel) {                                                                             \
