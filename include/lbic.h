@@ -133,6 +133,20 @@ int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 
+/* decompress() of n_teams batches at once (reference format; no reference counterpart for the batching: the
+ * reference decodes one image at a time, agents/blkbsdimgcomp_agent.py:591-599 -> net:400-452).  Batch t is decoded by
+ * handle ms[t] (distinct handles of one geometry, e.g. lbc_create_sibling) from streams[t * n_img + i] /
+ * lens[t * n_img + i] into zhat_devs[t]; results are bit-identical to lbc_decode of each batch.  All batches run
+ * in ONE persistent GPU launch (k_dec_team: one team of workgroups per batch, team barriers between the operations
+ * of a raster step).  Batches the team kernel does not cover (streams averaging >= 1 bit per symbol, M > 256) are
+ * decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
+int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *streams, const size_t *lens, int n_img,
+                    int Hb, int Wb, float *const *zhat_devs, void *stream);
+/* raw s_memrealtime stamps (100 MHz) of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 64 per team:
+ * [op] after each barrier of the sampled raster step (Hb/2, Wb/2), [60] end of the step before it, [61] end of the
+ * sampled step, [62] launch start, [63] launch end (team rank 0).  m = the call's first handle. */
+int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
+
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder
  * format as lbc_rans_encode.  Costs 12 bytes per block row over the reference format and lets the

@@ -178,6 +178,12 @@ struct lbc_model {
     int band_v0 = -1;
     std::map<std::pair<int, int>, hipGraphExec_t> band_exec;
     std::vector<long long> band_key;
+    // team decoder (lbc_decode_team, held by the first handle of a call): the recorded raster step of every
+    // team, the barrier words, and the stamps of the last launch
+    DevBuf team_prog, team_sync, team_ts;
+    std::vector<long long> team_key;
+    TeamArgs team_args{};
+    std::vector<unsigned long long> team_ts_host;
 };
 
 namespace {
@@ -409,8 +415,25 @@ int prof_range_begin(Prof* p, int r, hipStream_t s) {
     return LBC_OK;
 }
 
+// Recording mode (lbc_decode_team): gemm() prepares the arguments as launch_gemm would and appends them to the
+// program instead of launching; the team kernel replays them for every raster step.
+struct Recorder {
+    std::vector<GemmArgs> gemms;
+    std::vector<int> ops;     // >= 0: GEMM index, -1: the rANS decode
+};
+static thread_local Recorder* g_rec = nullptr;
+
 // launch a GEMM; in a sampled step give it a timing slot and record its algorithmic work
 int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
+    if (g_rec) {
+        GemmArgs g = g0;
+        if (g.M <= 0) return set_error(LBC_E_ARG, "empty GEMM in a recorded step");
+        const int rc = prepare_gemm(g);
+        if (rc) return rc;
+        g_rec->ops.push_back((int)g_rec->gemms.size());
+        g_rec->gemms.push_back(g);
+        return LBC_OK;
+    }
     Prof* p = g_prof;
     if (p) p->per_replay[p->range][gemm_class(g0)] += 1;   // the class launch_gemm will pick
     if (!p || !p->active) return launch_gemm(g0, s);
@@ -1241,6 +1264,179 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     HIPCHK(hipEventRecord(m->ev[3], s));
     m->dec_timed = true;
     return check_status(m, (size_t)n_img, s);
+}
+
+// ---------------------------------------------------------------------------------------------- team decode
+// lbc_decode_team: T batches (one per handle) decoded by ONE persistent k_dec_team launch, S workgroups per batch.
+// The raster step each team replays is recorded from the same run_ctx / run_dec calls that build the graph decoder
+// (three column classes: the KS3311 layer-0 cache computes border cells at h = 0 and h = Wb - 1), so the team
+// decoder computes exactly what lbc_decode computes.  Falls back to lbc_decode per batch where the team kernel does
+// not apply (dense rANS tables, M > 256, buffers past the 4 GB reach of its buffer loads, LBIC_TEAM=0).
+static std::mutex g_team_mu;   // one team launch at a time per process: its grid must be resident as a whole
+
+static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* streams, const size_t* lens, int n_img,
+                         int Hb, int Wb, float* const* zhat, void* stream) {
+    for (int t = 0; t < T; ++t) {
+        const int rc = lbc_decode(ms[t], streams + (size_t)t * n_img, lens + (size_t)t * n_img, n_img, Hb, Wb, zhat[t],
+                                  stream);
+        if (rc) return rc;
+    }
+    return LBC_OK;
+}
+
+int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* streams, const size_t* lens, int n_img,
+                    int Hb, int Wb, float* const* zhat_devs, void* stream) {
+    if (!ms || !streams || !lens || !zhat_devs) return set_error(LBC_E_ARG, "null argument");
+    if (n_teams < 1 || n_teams > TEAM_MAX) return set_error(LBC_E_ARG, "1 to 8 batches per team decode");
+    if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
+    const int T = n_teams;
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        if (!m || !zhat_devs[t]) return set_error(LBC_E_ARG, "null handle or output");
+        if (!m->finalized) return set_error(LBC_E_STATE, "lbc_finalize() not called");
+        if (!m->tabs_set) return set_error(LBC_E_NOT_UPDATED, "Uninitialized CDFs. Run update() first");
+        for (int u = 0; u < t; ++u)
+            if (ms[u] == m) return set_error(LBC_E_ARG, "every batch needs its own handle (lbc_create_sibling)");
+        if (m->B != ms[0]->B || m->N != ms[0]->N || m->M != ms[0]->M || m->P != ms[0]->P || m->l0_on != ms[0]->l0_on ||
+            m->cfg.device != ms[0]->cfg.device)
+            return set_error(LBC_E_ARG, "team decode handles must share one geometry and device");
+    }
+    const char* te = getenv("LBIC_TEAM");
+    const int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
+    const double zbytes = (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->Cx * 4;
+    const double lbytes = ms[0]->l0_on ? (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->C1P * 4 : 0.0;
+    if ((te && atoi(te) == 0) || !sparse || ms[0]->M > 256 || zbytes >= 4294967296.0 || lbytes >= 4294967296.0)
+        return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+    std::lock_guard<std::mutex> team_lock(g_team_mu);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    lbc_model* m0 = ms[0];
+    int rc;
+    int dev = m0->cfg.device, cus = 0;
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_cu = team_blocks_per_cu();
+    int S = std::min(32, cus / T);
+    if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
+    if (S < 1 || per_cu < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        if ((rc = prepare_device(m))) return rc;
+        if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+        if ((rc = m->ctr.alloc(kLanes * sizeof(int)))) return rc;
+        std::vector<std::pair<const uint8_t*, size_t>> subs;
+        for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[(size_t)t * n_img + i], lens[(size_t)t * n_img + i]);
+        if ((rc = upload_streams(m, subs, s))) return rc;
+    }
+    // the recorded program, rebuilt when any team's buffers or weights moved
+    std::vector<long long> key = {T, S, n_img, Hb, Wb};
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        for (long long x : {(long long)m->words.p, (long long)m->zpad.p, (long long)m->lane[0].ctx0.p,
+                            (long long)m->lane[0].d0.p, (long long)m->table_dev.p, (long long)m->tmeta_dev.p,
+                            (long long)m->st_x.p, (long long)m->l0.p, (long long)m->net->ctx0.W.p,
+                            (long long)m->net->d3.W.p})
+            key.push_back(x);
+    }
+    if (key != m0->team_key) {
+        std::vector<GemmArgs> gem;
+        std::vector<RansArgs> rans;
+        std::vector<int> ops;
+        int NG = -1;
+        for (int t = 0; t < T; ++t) {
+            lbc_model* m = ms[t];
+            Work& w = m->lane[0];
+            for (int c = 0; c < 3; ++c) {
+                const int hc = c == 0 ? 0 : c == 1 ? std::min(1, Wb - 1) : Wb - 1;
+                Recorder rec;
+                GemmArgs g = base_args(m, m->blocks_dec.as<int4>(), n_img, nullptr, n_img, Hb, Wb);
+                g.ctr = m->ctr.as<int>();
+                g.ctr_stride = Wb * n_img;
+                g.raster = 1;
+                g.raster_img0 = 0;
+                g.raster_h = hc;
+                g_rec = &rec;
+                int crc = run_ctx(m, w, g, true, nullptr);
+                rec.ops.push_back(-1);
+                if (!crc) crc = run_dec(m, w, g, nullptr);
+                g_rec = nullptr;
+                if (crc) return crc;
+                if (NG < 0) {
+                    NG = (int)rec.gemms.size();
+                    ops = rec.ops;
+                }
+                if ((int)rec.gemms.size() != NG || rec.ops != ops || (int)ops.size() > TEAM_MAXOPS)
+                    return set_error(LBC_E_STATE, "team decoder: raster steps differ in shape");
+                gem.insert(gem.end(), rec.gemms.begin(), rec.gemms.end());
+            }
+            RansArgs r = rans_args(m);
+            r.idx = w.idx.as<int32_t>();
+            r.ksi = w.ksi.as<float>();
+            r.yq = w.yq.as<float>();
+            r.rows = n_img;
+            r.sparse = 1;
+            rans.push_back(r);
+        }
+        const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
+        if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
+        HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
+        if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned)))) return rc;
+        if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 64 * sizeof(unsigned long long)))) return rc;
+        TeamArgs& a = m0->team_args;
+        a = TeamArgs{};
+        a.gemm = m0->team_prog.as<GemmArgs>();
+        a.rans = reinterpret_cast<const RansArgs*>(static_cast<char*>(m0->team_prog.p) + gb);
+        for (size_t i = 0; i < ops.size(); ++i) a.opk[i] = ops[i];
+        a.nops = (int)ops.size();
+        a.NG = NG;
+        a.T = T;
+        a.S = S;
+        a.Hb = Hb;
+        a.Wb = Wb;
+        a.sync = m0->team_sync.as<unsigned>();
+        m0->team_key = key;
+    }
+    TeamArgs a = m0->team_args;
+    a.tmo = 100000000ull;                    // 1 s at one barrier: far above any operation's time
+    const char* st = getenv("LBIC_TEAM_STAMPS");
+    a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
+    a.sv = Hb / 2;
+    a.sh = Wb / 2;
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+        if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s)))
+            return rc;
+    }
+    HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));
+    if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 64 * sizeof(unsigned long long), s));
+    HIPCHK(hipEventRecord(m0->ev[2], s));
+    if ((rc = launch_dec_team(a, s))) return rc;
+    HIPCHK(hipEventRecord(m0->ev[3], s));
+    m0->dec_timed = true;
+    for (int t = 0; t < T; ++t)
+        if ((rc = launch_copy_interior(ms[t]->zpad.as<float>(), zhat_devs[t], n_img, Hb, Wb, ms[t]->Cx, s))) return rc;
+    unsigned fail = 0;
+    HIPCHK(hipMemcpyAsync(&fail, m0->team_sync.as<unsigned>() + T * 32, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    if (a.ts) {
+        m0->team_ts_host.assign((size_t)T * 64, 0ull);
+        HIPCHK(hipMemcpyAsync(m0->team_ts_host.data(), m0->team_ts.p, (size_t)T * 64 * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (fail) return set_error(LBC_E_HIP, "team decoder: a workgroup gave up waiting at a barrier (grid not resident?)");
+    for (int t = 0; t < T; ++t)
+        if ((rc = check_status(ms[t], (size_t)n_img, s))) return rc;
+    return LBC_OK;
+}
+
+int lbc_team_stamps(const lbc_model* m, unsigned long long* out, int max_out, int* n_out) {
+    if (!m || !n_out) return set_error(LBC_E_ARG, "null argument");
+    const int n = (int)m->team_ts_host.size();
+    *n_out = n;
+    if (out)
+        for (int i = 0; i < n && i < max_out; ++i) out[i] = m->team_ts_host[i];
+    return LBC_OK;
 }
 
 static const uint32_t kRowsMagic = 0x3157424Cu;   // "LBW1"

@@ -157,13 +157,14 @@ int rans_decode_host(const EntropyTables& t, const uint8_t* data, size_t len, co
 //   fine   per table: e[0 .. len_t - 2], then 64 x 0xFFFF (so a 64-wide window never leaves the table)
 // S_t = ceil((len_t - 1) / 64) symbols per coarse segment; a table with len_t <= 64 is "short": its coarse
 // row is its whole CDF (S = 1).
-// meta [6][64]: fine row start (bytes), S (in bytes: 2 S), len - 2 (the escape symbol), coarse row start (bytes),
-// offset (-pmf_center).
+// meta [8][64]: fine row start (bytes), S (in bytes: 2 S), len - 2 (the escape symbol), coarse row start (bytes),
+// offset (-pmf_center), then the intervals lo | freq << 16 of the symbols of value 0, -1 and +1 (the sparse
+// decoder's compare-only paths).
 int build_rans_gpu_tables(const EntropyTables& t, std::vector<uint16_t>& img, std::vector<int>& meta) {
     const int nt = t.n_tables;
     if (nt < 1 || nt > 64) return set_error(LBC_E_ARG, "GPU rANS decoder supports 1..64 tables");
     img.assign((size_t)nt * 64, 0xFFFF);
-    meta.assign(6 * 64, 0);
+    meta.assign(8 * 64, 0);
     for (int i = 0; i < nt; ++i) {
         const int len = t.length[i];
         if (len < 3 || len > t.stride) return set_error(LBC_E_ARG, "bad cdf length");
@@ -187,9 +188,13 @@ int build_rans_gpu_tables(const EntropyTables& t, std::vector<uint16_t>& img, st
         // (freq < 2^16: the escape symbol always keeps a share), the sparse decoder's one-compare fast path
         const int c0 = -t.offset[i];
         if (c0 < 0 || c0 + 1 >= len - 1) return set_error(LBC_E_ARG, "cdf offset outside the table");
-        const int lo = cdf[c0], fr = cdf[c0 + 1] - cdf[c0];
-        if (lo > 0xFFFF || fr > 0xFFFF) return set_error(LBC_E_ARG, "bad centre interval");
-        meta[320 + i] = lo | (fr << 16);
+        for (int d = 0; d < 3; ++d) {     // value 0, -1, +1: index c0, c0 - 1, c0 + 1
+            const int c = d == 0 ? c0 : d == 1 ? c0 - 1 : c0 + 1;
+            if (c < 0 || c >= len - 2) continue;   // no such symbol, or the escape: freq 0 never matches
+            const int lo = cdf[c], fr = cdf[c + 1] - cdf[c];
+            if (lo > 0xFFFF || fr > 0xFFFF) return set_error(LBC_E_ARG, "bad centre interval");
+            meta[(5 + d) * 64 + i] = lo | (fr << 16);
+        }
     }
     while (img.size() & 7) img.push_back(0xFFFF);   // 16-byte granules for the LDS staging loads
     if (img.size() * 2 > 150 * 1024) return set_error(LBC_E_ARG, "cdf tables exceed the LDS budget");

@@ -78,9 +78,9 @@ struct GemmArgs {
 struct RansArgs {
     const uint16_t* cdf16;   // LDS image of the tables (build_rans_gpu_tables: coarse rows, then padded
                              // fine rows, entries stored as cdf - 1)
-    const int* tmeta;        // [6][64] per table: fine row start, 2 S (S = symbols per coarse lane), cdf_length - 2,
-                             // coarse row start (starts in bytes of the image), offset (-pmf_center), centre
-                             // interval of the value-0 symbol packed lo | freq << 16
+    const int* tmeta;        // [8][64] per table: fine row start, 2 S (S = symbols per coarse lane), cdf_length - 2,
+                             // coarse row start (starts in bytes of the image), offset (-pmf_center), intervals
+                             // of the value 0, -1, +1 symbols packed lo | freq << 16
     int total16;             // entries in cdf16 (multiple of 8)
     const uint32_t* words;   // concatenated streams
     const long long* word_base;
@@ -103,6 +103,26 @@ struct RansArgs {
     int sparse;              // 1: k_rans_decode_sparse (centre-interval fast path, tables read from global memory)
 };
 
+// Team decoder (k_dec_team, kernels.hip): the raster decodes of T batches in ONE persistent launch, S workgroups
+// per batch ("team"), team barriers between the recorded operations of a raster step instead of kernel boundaries
+constexpr int TEAM_MAX = 8;        // teams per launch
+constexpr int TEAM_MAXOPS = 24;    // operations per raster step
+struct TeamArgs {
+    const GemmArgs* gemm;    // [T][3][NG] prepared GEMMs of one raster step, per team and column class
+                             // (0: h = 0, 1: 0 < h < Wb - 1, 2: h = Wb - 1); block rows / columns set in-kernel
+    const RansArgs* rans;    // [T] (sparse decoder, one stream per image)
+    int opk[TEAM_MAXOPS];    // the step: >= 0 a GEMM index, -1 the rANS decode
+    int nops, NG, T, S, Hb, Wb;
+    unsigned* sync;          // [T][32] arrival counters (one 128-byte line each), then the failure word at [T * 32];
+                             // zeroed before every launch
+    unsigned long long tmo;  // s_memrealtime ticks (100 MHz) one barrier waits before the launch gives up
+    unsigned long long* ts;  // optional [T][64]: s_memrealtime after every barrier of raster step (sv, sh)
+    int sv, sh;
+};
+
+int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
+int launch_dec_team(const TeamArgs& a, hipStream_t s);
+int team_blocks_per_cu();          // k_dec_team workgroups one CU holds (occupancy query; 0 on error)
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
 int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = k_gemm
 int launch_rans_decode(const RansArgs& a, hipStream_t s);

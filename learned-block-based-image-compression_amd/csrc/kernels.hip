@@ -125,6 +125,21 @@ __device__ __forceinline__ float std_cum(float x) {
     return 0.5f * erfcf(-0.70710677f * x);
 }
 
+// Plain, or write-through (sc1) / L1-bypassing (sc1) global accesses: the team decoder (k_dec_team) hands every
+// value it writes to other workgroups of the same launch (cdna_hip_programming.md §6 Guideline 16, R1).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <bool SC1, typename T>
+__device__ __forceinline__ void st(T* p, T v) {
+    if constexpr (SC1) __hip_atomic_store((gptr<T>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <bool SC1, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (SC1) return __hip_atomic_load((gptr<T>)const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
 // Block (img, v, h) of A-row block m: from the block list, or computed for a decoder raster step
 // (GemmArgs::raster: img = img0 + m, v = the graph's row counter, h fixed), which saves the kernel one
 // dependent global load before its first activation load.
@@ -137,11 +152,12 @@ struct BlkSrc {
 // Output element (row, col) of a GEMM from its slice-ordered sum v: bias + the layer's epilogue.  Shared by
 // both GEMM kernels so that they compute bit-identical values.
 // bcol = bias[col]; xv = the GDN input x[row][col] (GDN / IGDN only), both loaded by the caller.
+template <bool SC1 = false>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const BlkSrc& blocks, float bcol,
                                          float xv) {
     switch (g.epi) {
         case EPI_BIAS:
-            g.out[(long)row * g.ldo + col] = v + bcol;
+            st<SC1>(g.out + (long)row * g.ldo + col, v + bcol);
             break;
         case EPI_LEAKY: {
             const float t = v + bcol;
@@ -158,7 +174,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
                 const int vv = b.y + dy, hh = b.z + dx;
                 if (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb) o = 0.f;
             }
-            g.out[(long)row * g.ldo + col] = o;
+            st<SC1>(g.out + (long)row * g.ldo + col, o);
             break;
         }
         case EPI_LEAKY_L0: {   // row = block * P + position -> the layer-0 cache cell of that position
@@ -174,14 +190,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             const int4 b = blocks.at(m);
             const int vv = b.y + dy, hh = b.z + dx;
             if (g.zero_oob && (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb)) o = 0.f;
-            g.out[(((long)b.x * g.geo.Hp + vv + 2) * g.geo.Wp + hh + 2) * g.ldo + col] = o;
+            st<SC1>(g.out + (((long)b.x * g.geo.Hp + vv + 2) * g.geo.Wp + hh + 2) * g.ldo + col, o);
             break;
         }
         case EPI_GDN:
         case EPI_IGDN: {
             const float norm = v + bcol;
             const float sq = __fsqrt_rn(norm);
-            g.out[(long)row * g.ldo + col] = g.epi == EPI_GDN ? xv * __fdiv_rn(1.0f, sq) : xv * sq;
+            st<SC1>(g.out + (long)row * g.ldo + col, g.epi == EPI_GDN ? xv * __fdiv_rn(1.0f, sq) : xv * sq);
             break;
         }
         case EPI_QUANT: {
@@ -191,33 +207,33 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             const float d = y - mean;
             const int sym = (int)rintf(d);               // torch.round: half to even
             const float yq = (float)sym + mean;
-            g.out[(long)row * g.ldo + col] = yq;
+            st<SC1>(g.out + (long)row * g.ldo + col, yq);
             const int4 b = blocks.at(row);
             const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
-            g.sym[pos] = sym;
-            g.idx[pos] = g.table ? scale_index(scale, g.table) : 0;   // no table: forward()/validation before update()
+            st<SC1>(g.sym + pos, (int32_t)sym);
+            st<SC1>(g.idx + pos, (int32_t)(g.table ? scale_index(scale, g.table) : 0));   // no table: forward()/validation before update()
             if (g.bits) {
                 const float av = fabsf(yq - mean), sb = fmaxf(scale, 0.11f);
                 const float lik = std_cum((0.5f - av) / sb) - std_cum((-0.5f - av) / sb);
-                g.bits[pos] = -log2f(fmaxf(lik, 1e-9f));
+                st<SC1>(g.bits + pos, -log2f(fmaxf(lik, 1e-9f)));
             }
             break;
         }
         case EPI_CTXIDX: {
             const float t = v + bcol;
-            g.out[(long)row * g.ldo + col] = t;
-            if (col < g.Mlat) g.idx[(long)row * g.Mlat + col] = scale_index(t, g.table);
+            st<SC1>(g.out + (long)row * g.ldo + col, t);
+            if (col < g.Mlat) st<SC1>(g.idx + (long)row * g.Mlat + col, (int32_t)scale_index(t, g.table));
             break;
         }
         case EPI_SCATTER: {   // output row of block (img, v, h) -> out[img][v][h][col] (forward()'s xhat)
             const int4 b = blocks.at(row);
-            g.out[((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col] = v + bcol;
+            st<SC1>(g.out + ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col, v + bcol);
             break;
         }
         case EPI_CLAMPZ: {
             const float t = fminf(fmaxf(v + bcol, -0.5f), 0.5f);
             const int4 b = blocks.at(row);
-            g.geo.zpad[((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col] = t;
+            st<SC1>(g.geo.zpad + ((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col, t);
             break;
         }
     }
@@ -625,8 +641,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     return launch_status("k_gemm");
 }
 
-int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
-    GemmArgs g = g0;
+int prepare_gemm(GemmArgs& g) {
     g.need_blocks = g.epi == EPI_QUANT || g.epi == EPI_CLAMPZ || g.epi == EPI_SCATTER || g.epi == EPI_LEAKY_L0 || g.zero_oob;
     for (int t = 0; t < g.nseg && t < MAXSEG; ++t) g.need_blocks |= g.seg[t].kind != SEG_DENSE;
     if (g.M <= 0) return LBC_OK;
@@ -651,6 +666,14 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         g.seg[t] = g.seg[0];
         g.seg[t].k0 = g.seg[t].k1 = 1 << 30;
     }
+    return LBC_OK;
+}
+
+int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
+    GemmArgs g = g0;
+    if (g.M <= 0) return LBC_OK;
+    int rc = prepare_gemm(g);
+    if (rc) return rc;
     if (gemm_class(g) == 0) {      // small M (the decoder's per-step batch, wavefront ramps): latency-shaped kernel
         if (cfg_id) *cfg_id = 0;
         dim3 grid((g.N + 15) / 16, (g.M + 15) / 16);
@@ -921,10 +944,13 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 // Sparse variant (low rates: almost every symbol is the most probable one, value 0).  No table image in LDS:
 // per symbol ONE compare of cum against the centre interval [lo, lo + freq) of the symbol's table (tmeta row
 // 5, gathered into a lane-per-symbol register in the prologue) decides; a hit costs the 64-bit state update
-// and nothing else.  A miss runs the two-level search of rans_row on the table image in global memory (the
-// 70 KB image stays L2-resident: every launch of every decoder reads it).  The prologue therefore needs only
+// and nothing else.  A miss compares against the intervals of values -1 and +1 (rows 6 and 7, SALU only), then
+// runs the two-level search of rans_row on the table image in global memory (the 70 KB image stays L2-resident:
+// every launch of every decoder reads it).  The prologue therefore needs only
 // the stream state, the block's indexes and the stream words -- no 70 KB LDS fill and no workgroup barrier
 // for it -- and each wave is independent.  Bit-identical to rans_row (same coder, same tables).
+// SC1: inside k_dec_team (indexes and means from the context net's workgroups, y_qnt to the decoder's)
+template <bool SC1 = false>
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane) {
     RSTAMP(0);
     const bool valid = row_in < a.rows;
@@ -939,13 +965,14 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     const int Mlat = a.Mlat;
     const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
     const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane], t_lf = a.tmeta[320 + lane];
+    const int t_lfm = a.tmeta[384 + lane], t_lfp = a.tmeta[448 + lane];
     const unsigned long long x_in = a.state_x[img];
     const int p_in = a.state_ptr[img];
     const long long wb = a.word_base[img];
     const int nw_in = a.word_count[img];
     int ti[4];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) ti[kb] = a.idx[(long)row * Mlat + min(kb * 64 + lane, Mlat - 1)] & 63;
+    for (int kb = 0; kb < 4; ++kb) ti[kb] = ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1)) & 63;
     unsigned long long x = uni64(x_in);
     int p = __builtin_amdgcn_readfirstlane(p_in);
     const uint32_t* w = a.words + wb;
@@ -959,13 +986,15 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         for (int k = 0; k < RANS_WIN / 64; ++k) lwin[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
     }
     // lane i of chunk kb = symbol 64 kb + i: its centre interval (lo, freq), table metadata and offset
-    int lov[4], frv[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
+    int lov[4], frv[4], ivm[4], ivp[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int sel = ti[kb] << 2;
         const int lf = __builtin_amdgcn_ds_bpermute(sel, t_lf);
         lov[kb] = lf & 0xffff;
         frv[kb] = (int)((uint32_t)lf >> 16);
+        ivm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lfm);
+        ivp[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lfp);
         sfb[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
         sS[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
         slm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
@@ -1041,8 +1070,22 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
             }
             while (ii < cnt_i && fast(rdlane((uint32_t)lov[kb], ii), rdlane((uint32_t)frv[kb], ii))) ++ii;
             if (ii >= cnt_i) break;
-            // another symbol: the two-level search of rans_row on the table image in global memory
             const uint32_t cum = (uint32_t)x & 0xffffu;
+            // value -1 or +1 (most of the misses): two more interval compares, no memory access
+            {
+                const uint32_t im = rdlane((uint32_t)ivm[kb], ii), ip = rdlane((uint32_t)ivp[kb], ii);
+                const uint32_t dm = cum - (im & 0xffffu), dp = cum - (ip & 0xffffu);
+                const bool hm = dm < (im >> 16), hp = dp < (ip >> 16);
+                if (hm || hp) {
+                    const uint32_t fr = hm ? im >> 16 : ip >> 16, d = hm ? dm : dp;
+                    x = (unsigned long long)fr * (x >> 16) + d;
+                    renorm();
+                    symv[kb] = lane == ii ? symv[kb] + (hm ? -1 : 1) : symv[kb];
+                    ++ii;
+                    continue;
+                }
+            }
+            // another symbol: the two-level search of rans_row on the table image in global memory
             const int fb = rdlane_i(sfb[kb], ii), S = rdlane_i(sS[kb], ii);
             const int lm2 = rdlane_i(slm[kb], ii), ca = rdlane_i(sca[kb], ii);
             const uint32_t cv = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + ca + lane2);
@@ -1083,7 +1126,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         const int i = kb * 64 + lane;
         if (i < Mlat) {
             if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
-            else a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
+            else st<SC1>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + ld<SC1>(a.ksi + (long)row * a.ldk + Mlat + i));
         }
     }
     if (lane == 0) {
@@ -1132,6 +1175,280 @@ int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     const int wpb = a.rows < RANS_WPB ? a.rows : RANS_WPB;
     hipLaunchKernelGGL(k_rans_decode, dim3((a.rows + RANS_WPB - 1) / RANS_WPB), dim3(wpb * 64), lds, s, a);
     return launch_status("k_rans_decode");
+}
+
+// ----------------------------------------------------------------------------------------- team decoder
+// k_dec_team: the reference-format raster decodes of T batches in ONE persistent launch.  Team t = the S
+// workgroups with blockIdx % T == t decodes batch t (with T = 8 a team's workgroups share one XCD under the
+// observed round-robin placement: speed only, nothing depends on it).  A team runs its batch's raster steps with
+// the operations the graph decoder launches -- context net x 4, rANS, decoder x 7, recorded by the host as
+// prepared GemmArgs / RansArgs -- and a team barrier between operations instead of a kernel boundary: a raster
+// step of 12 dependent launches pays 12 barriers (one agent-scope arrival per workgroup, one polling lane) in
+// place of 12 launch boundaries, and T chains run side by side in one launch instead of one per hardware queue
+// (at most four overlap: DESIGN.md §5).
+// Hand-offs follow cdna_hip_programming.md §6 Guideline 16, R1: every value a workgroup writes for the others
+// (activations, scale indexes, y_qnt, the reconstruction and the layer-0 cache) is stored sc1 (write-through),
+// every storing wave drains (vmcnt(0)) before its workgroup's single arrival, and every load of such a value is an
+// sc1 load (buffer_load ... sc1 for the GEMM A operand, global sc1 loads for the GDN inputs and the rANS inputs);
+// weights, biases and the tables are read-only.  Every spin is bounded (TeamArgs::tmo): a workgroup that gives up
+// sets the failure word, which every other waiter reads, so the whole grid drains and the host reports an error.
+// GEMM arithmetic per output element is k_gemm_s's (KSPLIT slices, the same MFMA chains, the slice-ordered sum,
+// the shared epilogue): results are bit-identical to the graph decoder's.
+
+// A fragment of k-block kb through an sc1 (L1-bypassing) buffer load; byte offsets < 4 GB (host-checked)
+__device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
+    const int k = kb << 4;
+    gfloat_p base = rw.base[0];
+    unsigned o = rw.off[0];
+#pragma unroll
+    for (int t = 1; t < MAXSEG; ++t) {
+        const bool in = k >= rw.k0[t];
+        base = in ? rw.base[t] : base;
+        o = in ? rw.off[t] : o;
+    }
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, -1, 0x00020000);
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (o + (unsigned)(k >> 2)) << 4, 0, 16));
+}
+
+// one GEMM of the step, this workgroup's share: output tiles (row tile mt, column tile nt) = item i = nt * MT + mt,
+// items rank, rank + S, ...; the weight fragments of the next item are requested before the current item's chain
+template <int L, bool EXACT>
+__device__ __forceinline__ void team_gemm(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
+    constexpr int LL = EXACT ? L : L + 1;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
+    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
+    if (rank >= items) return;
+    const BlkSrc blocks{nullptr, 1, 0, v, h};
+    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
+    f4 a[LL], w0[LL], w1[LL];
+    float b0 = 0.f, x0 = 0.f, b1 = 0.f, x1 = 0.f;
+    int amt = -1, buf = 0;
+    auto issue = [&](int it, f4 (&w)[LL], float& bb, float& xx) {
+        const int mt = it % MT, nt = it / MT;
+        const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
+        bb = g.bias[ecol];
+        xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+#pragma unroll
+        for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
+    };
+    auto load_a = [&](int mt) {
+        const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
+#pragma unroll
+        for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
+        amt = mt;
+    };
+    auto run = [&](int it, f4 (&w)[LL], float bb, float xx) {
+        const int mt = it % MT, nt = it / MT;
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < LL; ++c) {
+            f4 av = a[c];
+            if (g.square_a) av = av * av;
+            f4 t = acc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+            acc = c < n ? t : acc;
+        }
+        float* rb = red + buf * (KSPLIT * 256);
+        buf ^= 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only: the next item's weight loads stay in flight
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x < 256) {
+            const int e = threadIdx.x;
+            float vv = rb[e];
+#pragma unroll
+            for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
+            const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
+            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx);
+        }
+    };
+    int it = rank;
+    issue(it, w0, b0, x0);
+    load_a(it % MT);
+    while (true) {           // two named weight buffers, statically indexed
+        int nx = it + S;
+        if (nx < items) issue(nx, w1, b1, x1);
+        run(it, w0, b0, x0);
+        if (nx >= items) break;
+        if (nx % MT != amt) load_a(nx % MT);
+        it = nx;
+        nx = it + S;
+        if (nx < items) issue(nx, w0, b0, x0);
+        run(it, w1, b1, x1);
+        if (nx >= items) break;
+        if (nx % MT != amt) load_a(nx % MT);
+        it = nx;
+    }
+}
+
+// K beyond 8 x 12 k-blocks: each item's slice in chunks of 12 k-blocks, A and weights per chunk, no prefetch
+__device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
+    constexpr int CH = 12;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
+    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
+    const BlkSrc blocks{nullptr, 1, 0, v, h};
+    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
+    int buf = 0;
+    for (int it = rank; it < items; it += S) {
+        const int mt = it % MT, nt = it / MT;
+        const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
+        const float bb = g.bias[ecol];
+        const float xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+        const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        for (int c0 = kb0; c0 < kb1; c0 += CH) {
+            const int cn = min(CH, kb1 - c0);
+            f4 a[CH], w[CH];
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int kb = min(c0 + c, nkb - 1);
+                w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
+                a[c] = small_a_sc1(rw, kb);
+            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                f4 av = a[c];
+                if (g.square_a) av = av * av;
+                f4 t = acc;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+                acc = c < cn ? t : acc;
+            }
+        }
+        float* rb = red + buf * (KSPLIT * 256);
+        buf ^= 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x < 256) {
+            const int e = threadIdx.x;
+            float vv = rb[e];
+#pragma unroll
+            for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
+            const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
+            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx);
+        }
+    }
+}
+
+__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
+    const int nkb = g.K >> 4;
+    const int L = nkb / KSPLIT;
+    const bool exact = (nkb % KSPLIT) == 0;
+    switch (L) {
+#define LBIC_T(L_)                                                                                 \
+    case L_:                                                                                       \
+        if (exact) team_gemm<L_, true>(g, v, h, rank, S, red);                                     \
+        else team_gemm<L_, false>(g, v, h, rank, S, red);                                          \
+        break;
+        case 0: team_gemm<0, false>(g, v, h, rank, S, red); break;
+        LBIC_T(1) LBIC_T(2) LBIC_T(3) LBIC_T(4) LBIC_T(5) LBIC_T(6)
+        LBIC_T(7) LBIC_T(8) LBIC_T(9) LBIC_T(10) LBIC_T(11)
+#undef LBIC_T
+        default: team_gemm_long(g, v, h, rank, S, red);
+    }
+}
+
+// team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
+// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else)
+__device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
+                                          int* sflag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int f = 0;
+        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                f = 1;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                __hip_atomic_store((gptr<unsigned>)fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sflag = f;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
+    return *sflag == 0;
+}
+
+__global__ __launch_bounds__(512) void k_dec_team(const TeamArgs ta) {
+    __shared__ __attribute__((aligned(16))) float red[2 * KSPLIT * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
+    __shared__ int sflag;
+    const int T = ta.T, S = ta.S;
+    const int team = blockIdx.x % T, rank = blockIdx.x / T;
+    if (rank >= S) return;
+    unsigned* ctr = ta.sync + team * 32;
+    unsigned* fail = ta.sync + T * 32;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the recorded operations are read-only for the launch: constant address space, so their fields come in by
+    // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
+    typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
+    typedef const __attribute__((address_space(4))) RansArgs* crans_p;
+    const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
+    const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
+    unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 64 : nullptr;
+    if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
+    unsigned target = 0;
+    for (int v = 0; v < ta.Hb; ++v) {
+        for (int h = 0; h < ta.Wb; ++h) {
+            const int cls = h == 0 ? 0 : h == ta.Wb - 1 ? 2 : 1;
+            const bool samp = ts && v == ta.sv && h == ta.sh;
+            for (int op = 0; op < ta.nops; ++op) {
+                const int k = ta.opk[op];
+                if (k >= 0) {
+                    team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + k), v, h, rank, S, red);
+                } else if (wave == 0) {
+                    for (int r = rank; r < R.rows; r += S) rans_row_sparse<true>(R, lwin, r, lane);
+                }
+                target += S;
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
+                if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
+            }
+            if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
+            if (ts && v == ta.sv && h == ta.sh - 1 && threadIdx.x == 0) ts[60] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
+}
+
+int team_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team), 512, 0) != hipSuccess)
+        return 0;
+    return nb;
+}
+
+int launch_dec_team(const TeamArgs& a, hipStream_t s) {
+    if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
+        return set_error(LBC_E_ARG, "bad team decoder arguments");
+    hipLaunchKernelGGL(k_dec_team, dim3(a.T * a.S), dim3(512), 0, s, a);
+    return launch_status("k_dec_team");
 }
 
 __global__ void k_ctr_add(int* c, int d) { *c += d; }

@@ -45,6 +45,10 @@ _SIGS = {
                              ctypes.c_int, _P, _P], ctypes.c_int),
     "lbc_decode": ([_P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                     ctypes.c_int, _P, _P], ctypes.c_int),
+    "lbc_decode_team": ([ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t),
+                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P), _P], ctypes.c_int),
+    "lbc_team_stamps": ([_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
+                        ctypes.c_int),
     "lbc_encode_ex": ([_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int, _P],
                       ctypes.c_int),
     "lbc_set_option": ([_P, ctypes.c_int, ctypes.c_longlong], ctypes.c_int),

@@ -228,6 +228,17 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(fn(self._h, arr, lens, n, Hb, Wb, _lib.ptr(zhat), ctypes.c_void_p(stream)))
         return zhat
 
+    def team_stamps(self):
+        """Raw 100 MHz stamps of the last decompress_teams launch led by this handle (LBIC_TEAM_STAMPS=1), [T, 64]
+        (lbc_team_stamps): [op] after each barrier of the sampled raster step, 60/61 the ends of the step before it
+        and of the sampled step, 62/63 launch start / end."""
+        L = _lib.lib()
+        n = ctypes.c_int(0)
+        _lib.check(L.lbc_team_stamps(self._h, None, 0, ctypes.byref(n)))
+        buf = (ctypes.c_ulonglong * max(n.value, 1))()
+        _lib.check(L.lbc_team_stamps(self._h, buf, n.value, ctypes.byref(n)))
+        return [list(buf[i:i + 64]) for i in range(0, n.value, 64)]
+
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]
         int32 (chunk c = the next M symbols of every stream, as one raster step of decompress) ->
@@ -328,3 +339,27 @@ class BlockBasedImgCompLossyNetv9:
             raise ValueError("xshape must be [1, 3B^2, H/B, W/B]")
         z = self.decompress_batch([bitstream], hg, wd)
         return z.permute(0, 3, 1, 2).contiguous()
+
+
+def decompress_teams(models: Sequence["BlockBasedImgCompLossyNetv9"], batches: Sequence[Sequence[bytes]], Hb: int, Wb: int):
+    """Decode len(batches) <= 8 batches of reference-format bitstreams in ONE persistent launch (lbc_decode_team):
+    batch t by models[t] (distinct handles of one geometry, e.g. siblings), each batch the same number of images of
+    Hb x Wb blocks.  Returns [zhat_t [n, Hb, Wb, 3B^2]], bit-identical to models[t].decompress_batch(batches[t])."""
+    T = len(batches)
+    if T < 1 or T > 8 or len(models) < T:
+        raise ValueError("1 to 8 batches, one model handle each")
+    n = len(batches[0])
+    if any(len(b) != n for b in batches):
+        raise ValueError("every batch needs the same number of images")
+    for m in models[:T]:
+        m._check_ready()
+    bufs = [s if isinstance(s, bytes) else bytes(s) for b in batches for s in b]
+    arr = (ctypes.c_void_p * len(bufs))(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+    lens = (ctypes.c_size_t * len(bufs))(*[len(b) for b in bufs])
+    dev = models[0].device
+    zh = [torch.empty((n, Hb, Wb, models[0].arch.cx), dtype=torch.float32, device=dev) for _ in range(T)]
+    hs = (ctypes.c_void_p * T)(*[m._h for m in models[:T]])
+    zp = (ctypes.c_void_p * T)(*[_lib.ptr(z) for z in zh])
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.lib().lbc_decode_team(hs, T, arr, lens, n, Hb, Wb, zp, ctypes.c_void_p(stream)))
+    return zh

@@ -1,0 +1,120 @@
+"""Team decoder (lbc_decode_team / k_dec_team): several batches decoded by ONE persistent launch, one team of
+workgroups per batch, must reproduce the graph decoder (lbc_decode, itself bit-exact against the encoder and the
+reference's closed loops in test_gpu_parity.py) bit for bit: every geometry class of the recorded raster step
+(KS3111, KS3311 with the layer-0 cache's border classes), ragged frames, image counts that do not fill a 16-row
+tile or need three row tiles, tiny teams (many output tiles per workgroup: the weight-prefetch loop), corrupt
+streams, and the fallback for streams the team kernel does not take."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_arch, load_golden
+from lbic.weights import synth_state_dict
+
+pytestmark = pytest.mark.gpu
+
+_M = {}
+
+
+def handles(name, T):
+    """T sibling handles (one per batch) of the fixture's architecture and weights."""
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    if name not in _M:
+        cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
+        m = BlockBasedImgCompLossyNetv9(cfg)
+        m.load_state_dict(synth_state_dict(arch, int(g["weight_seed"])))
+        m.update(force=True)
+        _M[name] = [m]
+    hs = _M[name]
+    while len(hs) < T:
+        hs.append(hs[0].sibling())
+    return arch, hs[:T]
+
+
+def batches(arch, T, n, Hb, Wb, seed, scale=0.5):
+    rng = np.random.default_rng(seed)
+    return [torch.from_numpy((rng.random((n, Hb, Wb, arch.cx), dtype=np.float32) - 0.5) * scale * 2).cuda()
+            for _ in range(T)]
+
+
+def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05):
+    """Encode T batches, decode them by the graph decoder and by one team launch; return both."""
+    from lbic.model import decompress_teams
+    arch, hs = handles(name, T)
+    xs = batches(arch, T, n, Hb, Wb, seed, scale)
+    rs = [hs[0].compress_batch(x) for x in xs]
+    st = [hs[0].entropy_encode(r["symbols"], r["indexes"]) for r in rs]
+    ref = [hs[0].decompress_batch(s, Hb, Wb) for s in st]
+    for r, z in zip(rs, ref):
+        assert torch.equal(r["zhat"], z)
+    got = decompress_teams(hs, st, Hb, Wb)
+    return ref, got, hs, st
+
+
+@pytest.mark.parametrize("name,T,n,shape", [
+    ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
+    ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)),
+])
+def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
+    g = load_golden("loop_" + name)
+    Hb, Wb = shape or g["x"].shape[:2]
+    ref, got, _, _ = run_case(name, T, n, Hb, Wb, seed=T * 7 + n)
+    for t in range(T):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 9), (7, 1), (3, 5), (2, 2)])
+def test_team_ragged_frames_ks3311(shape, monkeypatch):
+    """One block, one row, one column, odd rectangles: the three column classes of the KS3311 step (layer-0 cache
+    border cells at h = 0 and h = Wb - 1, both at once when Wb = 1)."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    ref, got, _, _ = run_case("tiny_ks3311", 3, 2, *shape, seed=sum(shape))
+    for t in range(3):
+        assert torch.equal(got[t], ref[t])
+
+
+@pytest.mark.parametrize("S", [1, 3, 7])
+def test_team_small_teams(S, monkeypatch):
+    """Teams of 1, 3 and 7 workgroups: every workgroup walks many output tiles per GEMM (the weight-prefetch loop,
+    row tiles changing between items) and decodes several rANS streams per step."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_S", str(S))
+    ref, got, _, _ = run_case("b8_lowrate_2rows", 2, 35, 2, 6, seed=S)
+    for t in range(2):
+        assert torch.equal(got[t], ref[t])
+
+
+def test_team_fallback_and_errors(monkeypatch):
+    """Streams the team kernel does not take (dense rANS variant, LBIC_TEAM=0) decode through lbc_decode with the
+    same results; a truncated stream raises; the handles work afterwards."""
+    from lbic.model import decompress_teams
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
+    ref, got, hs, st = run_case("tiny_ks3111", 2, 3, 4, 5, seed=3)
+    for t in range(2):
+        assert torch.equal(got[t], ref[t])
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    bad = [list(st[0]), list(st[1])]
+    bad[1][2] = bad[1][2][:8]
+    with pytest.raises((ValueError, RuntimeError)):
+        decompress_teams(hs, bad, 4, 5)
+    with pytest.raises((ValueError, RuntimeError)):
+        decompress_teams([hs[0], hs[0]], st, 4, 5)     # one handle twice
+    got = decompress_teams(hs, st, 4, 5)
+    for t in range(2):
+        assert torch.equal(got[t], ref[t])
+
+
+def test_team_stamps(monkeypatch):
+    """LBIC_TEAM_STAMPS=1 records the sampled step's barrier times and the launch span per team."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_STAMPS", "1")
+    _, _, hs, _ = run_case("tiny_ks3111", 2, 4, 4, 6, seed=5)
+    ts = hs[0].team_stamps()
+    assert len(ts) == 2
+    for row in ts:
+        assert row[63] > row[62] > 0 and row[61] > row[60] > 0
