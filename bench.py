@@ -79,6 +79,10 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
     ap.add_argument("--share-weights", type=int, default=1,
                     help="1: decoder handles share the encoder handle's device weights (lbc_create_sibling)")
+    ap.add_argument("--team", type=int, default=8,
+                    help="headline schedule: one encoder handle compresses the batches while groups of TEAM encoded "
+                         "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
+                         "workgroups per 32-frame batch); 0 = the --workers / --depth schedules")
     ap.add_argument("--workers", type=int, default=4,
                     help="headline schedule: W workers, each (own handle + stream + thread) compressing, entropy coding "
                          "and decoding whole batches (0 = the encoder + --depth decoders pipeline)")
@@ -211,7 +215,7 @@ def main():
         return m
 
     depth = max(args.depth, 0)
-    ndec = max(depth, 2 if args.gang else 1, args.workers - 1, 1)
+    ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
     s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
     enc_model = make_model()
@@ -289,7 +293,9 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0):
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, plain=[])
+
+    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
         (or `gang` batches in one wavefront pass) while a helper thread entropy codes the previous one and
         `depth` decoder threads each decode `gang` queued batches per raster pass (their own handles and
@@ -304,11 +310,71 @@ def main():
         done = dict(count=0, last=None)      # only the latest batch is kept (its pinned / device buffers)
 
         def finish(k_, r_, st_, z_):
+            # the latest batch with a record (the team schedule keeps the record of the last batch only)
             with plock:
                 done["count"] += 1
-                if done["last"] is None or k_ > done["last"][0]:
+                cur = done["last"]
+                if cur is None or ((r_ is not None) == (cur[1] is not None) and k_ > cur[0]) or \
+                        (r_ is not None and cur[1] is None):
                     done["last"] = (k_, r_, st_, z_)
-        if workers:
+        if team:
+            # the encoder handle compresses batch after batch on its stream (host rANS on helper threads); a decoder
+            # thread takes the encoded batches in groups of `team` and decodes each group in ONE persistent launch
+            # (one team of workgroups per batch) on its own stream, beside the encoder's next batches
+            from concurrent.futures import ThreadPoolExecutor
+            from lbic.model import decompress_teams
+            dq = queue.Queue(maxsize=2 * team)
+            if prof:
+                for kk in team_acc:
+                    team_acc[kk] = [] if kk == "plain" else 0
+            errs = []
+
+            def team_decoder():
+                pend = []
+                try:
+                    while True:
+                        it = dq.get()
+                        if it is not None:
+                            pend.append(it)
+                        if pend and (it is None or len(pend) == team):
+                            t0_ = time.perf_counter()
+                            sts = [f_.result() for (_, _, f_) in pend]
+                            with torch.cuda.stream(s_decs[0]):
+                                zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb)
+                                s_decs[0].synchronize()
+                            with plock:
+                                ph["decode"] += time.perf_counter() - t0_
+                            if prof:
+                                st_ = dec_models[0].team_stats()
+                                team_acc["launches"] += 1
+                                team_acc["ms"] += st_["launch_ms"]
+                                team_acc["bytes"] += st_["bytes"]
+                                team_acc["flops"] += st_["flops"]
+                                team_acc["plain"].append(st_["plain"])
+                            for (k_, r_, _), st_, z_ in zip(pend, sts, zs):
+                                finish(k_, r_, st_, z_)
+                            pend = []
+                        if it is None:
+                            return
+                except BaseException as e:    # surfaced by the encoder thread below
+                    errs.append(e)
+                    while dq.get() is not None:
+                        pass
+
+            dth = threading.Thread(target=team_decoder)
+            dth.start()
+            with ThreadPoolExecutor(max_workers=4) as ex:
+                for k in range(steps):
+                    r_ = compress_side(ph, frames_of(base + k))
+                    f_ = ex.submit(entropy_side, r_, fmt, ph)
+                    # only the last batch keeps its record (zhat, symbols) for the quality check
+                    dq.put((base + k, r_ if k == steps - 1 else None, f_))
+                    del r_
+                dq.put(None)
+                dth.join()
+            if errs:
+                raise errs[0]
+        elif workers:
             # every worker (its own handle + stream) takes the next batch and compresses, entropy codes and decodes it
             wk = list(zip([enc_model] + dec_models, [s_enc] + s_decs))[:workers]
             nxt = dict(k=0)
@@ -422,23 +488,25 @@ def main():
     scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
     r0 = compress_side(scratch, frames_of(0))
     st0 = entropy_side(r0, "reference", scratch)
-    for i in range(len(dec_models)):
-        decode_side(i, st0, "reference", scratch)
-    if args.workers:       # every worker handle encodes too: build its encoder graph
+    if not args.team:
+        for i in range(len(dec_models)):
+            decode_side(i, st0, "reference", scratch)
+    if args.workers and not args.team:       # every worker handle encodes too: build its encoder graph
         for m_, s_ in list(zip(dec_models, s_decs))[:args.workers - 1]:
             compress_side(scratch, frames_of(0), m_, s_)
     if args.warmup > 0:
-        pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup", workers=args.workers)
+        pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup", workers=args.workers, team=args.team)
 
     # ---- headline: the reference bitstream format, one 32-frame batch per decode pass
-    dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline", workers=args.workers)
+    dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline", workers=args.workers,
+                                                  team=args.team)
 
     side = {}
-    if args.side_steps > 0 and depth != 1:
+    if args.side_steps > 0 and (depth != 1 or args.team or args.workers):
         d_, p_, _, _ = pipeline(args.side_steps, 1, label="one decode in flight")
         side["one_decode_in_flight"] = summary(d_, p_, args.side_steps, frames_in_flight_per_decode_pass=n,
                                                decode_passes_in_flight=1)
-    if args.side_steps > 0 and depth != 0:
+    if args.side_steps > 0 and (depth != 0 or args.team or args.workers):
         d_, p_, _, _ = pipeline(args.side_steps, 0, label="serial")
         side["serial_schedule"] = summary(d_, p_, args.side_steps)
     gang_s = None
@@ -483,7 +551,7 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = world * n * H * W / (dt / args.steps) / 1e6
 
-    roof, kernels = roofline(kstats, dt)
+    roof, kernels = roofline(kstats, dt, team_acc if args.team else None)
     mac_enc, mac_dec = arch.live_macs_per_block()
     step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
     cpu = None
@@ -500,12 +568,19 @@ def main():
         "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
                                f"in the reference bitstream format (one raster rANS stream per image); each decode pass "
                                f"decodes one {n}-frame batch ({n} frames in flight per pass), "
-                               + (f"up to {args.workers} passes in flight (one per worker)" if args.workers else
+                               + (f"up to {args.team} passes in flight (one team of workgroups per batch in one persistent "
+                                  "launch)" if args.team else
+                                  f"up to {args.workers} passes in flight (one per worker)" if args.workers else
                                   f"{depth} pass(es) in flight beside the encoder"),
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
                    "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
-                   "decode_passes_in_flight": args.workers or depth, "frames_per_encode_pass": n,
-                   "schedule": (f"workers: {args.workers} codec handles on one weight set, each with its own HIP stream "
+                   "decode_passes_in_flight": args.team or args.workers or depth, "frames_per_encode_pass": n,
+                   "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
+                                f"helper threads; every {args.team} encoded batches are decoded by ONE persistent "
+                                "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "
+                                "32-frame batch, team barriers instead of kernel boundaries), beside the next encodes"
+                                if args.team else
+                                f"workers: {args.workers} codec handles on one weight set, each with its own HIP stream "
                                 "and host thread, take the batches in turn and compress, entropy code (host rANS) and "
                                 "decode each whole batch" if args.workers else
                                 "serial: encode, entropy, decode per batch" if depth == 0 else
@@ -544,25 +619,34 @@ def gather_records(rec, ok, dist):
     return torch.cat(allrec), bool(flag.item() == 1.0)
 
 
-def roofline(kstats, dt):
-    """Dominant kernel family (sampled mean launch period x true launch count over the timed region) against
-    its roofline.  Durations are the in-kernel timing stamps of the sampled launches executed in the timed
-    region (lbc_profile_*): `avg_launch_us` is the launch-to-launch period in the stream chain (end of the
-    previous launch -> end of this one: the launch's span plus the boundary in front of it, which is what a
-    dispatch-to-completion trace measures), `avg_span_us` the workgroups' own span."""
-    if not kstats:
-        return None, {}
-    kernels = {}
-    for name, s in kstats.items():
+def roofline(kstats, dt, team=None):
+    """Dominant kernel family (its time share of the timed region) against its roofline.  Graph-launched kernels:
+    the in-kernel timing stamps of the sampled launches executed in the timed region (lbc_profile_*):
+    `avg_launch_us` is the launch-to-launch period in the stream chain (end of the previous launch -> end of this
+    one: the launch's span plus the boundary in front of it, which is what a dispatch-to-completion trace measures),
+    `avg_span_us` the workgroups' own span; share = period x true launch count.  The team decoder (`team`, one
+    persistent launch per group of batches): HIP events around each launch, algorithmic bytes / FLOPs per launch from
+    the library (lbc_team_stats)."""
+    kernels, fam = {}, {}
+    for name, s in (kstats or {}).items():
         span = s["total_ms"] / max(s["launches"], 1)
         per = s["total_ms_chain"] / s["launches_chain"] if s["launches_chain"] else span
         kernels[name] = dict(launches_sampled=int(s["launches"]), launches_total=int(s["total_launches"]),
                              avg_span_us=round(span * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
                              est_share_of_step=round(per * s["total_launches"] / 1e3 / dt, 4))
+        fam[name] = (s["flops"] / max(s["launches"], 1), s["bytes"] / max(s["launches"], 1))
+    if team and team["launches"]:
+        per = team["ms"] / team["launches"]
+        kernels["k_dec_team"] = dict(launches_sampled=team["launches"], launches_total=team["launches"],
+                                     avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
+                                     est_share_of_step=round(team["ms"] / 1e3 / dt, 4),
+                                     plain_handoffs=team["plain"], timing="HIP events around each launch")
+        fam["k_dec_team"] = (team["flops"] / team["launches"], team["bytes"] / team["launches"])
+    if not kernels:
+        return None, {}
     dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_total"])
-    s = kstats[dom]
     per_launch_s = kernels[dom]["avg_launch_us"] * 1e-6
-    fl, by = s["flops"] / s["launches"], s["bytes"] / s["launches"]
+    fl, by = fam[dom]
     ai = fl / by if by else float("inf")
     ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
     if fl > 0 and ai >= ridge:
@@ -571,12 +655,12 @@ def roofline(kstats, dt):
         ach, peak, unit, bound = by / per_launch_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile):       # rocprofv3 PMC passes of this command (tools/gpu_profile.sh)
+    if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/gpu_profile.sh, tools/team_pmc.sh)
         with open(tfile) as fh:
             pm = json.load(fh)
-        fam = re.sub(r"<.*>$", "", dom)
-        if fam in pm and "hbm_bytes_per_dispatch" in pm[fam]:
-            traffic = round(pm[fam]["hbm_bytes_per_dispatch"])
+        f_ = re.sub(r"<.*>$", "", dom)
+        if f_ in pm and "hbm_bytes_per_dispatch" in pm[f_]:
+            traffic = round(pm[f_]["hbm_bytes_per_dispatch"])
     roof = dict(kernel=dom, bound=bound, achieved=round(ach, 4), peak=peak, unit=unit, frac=round(ach / peak, 5),
                 traffic=traffic, avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],
                 algorithmic_per_launch=dict(flops=round(fl), bytes=round(by)), arithmetic_intensity=round(ai, 2),

@@ -142,10 +142,16 @@ int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, 
  * decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
 int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *streams, const size_t *lens, int n_img,
                     int Hb, int Wb, float *const *zhat_devs, void *stream);
-/* raw s_memrealtime stamps (100 MHz) of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 64 per team:
- * [op] after each barrier of the sampled raster step (Hb/2, Wb/2), [60] end of the step before it, [61] end of the
- * sampled step, [62] launch start, [63] launch end (team rank 0).  m = the call's first handle. */
+/* raw stamps of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 256 per team (team rank 0), s_memrealtime
+ * (100 MHz): [op] after each barrier of the sampled raster step (Hb/2, Wb/2), [32 + op] when rank 0's own share of the
+ * operation was done, [60] end of the step before it, [61] end of the sampled step, [62] launch start, [63] launch
+ * end; s_memtime (shader clock) [64 + 8 op + p] inside the operation's GEMM (p: entry, loads issued, first chain, all
+ * chains, outputs written).  m = the call's first handle. */
 int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
+/* the last lbc_decode_team launch led by m: its duration (HIP events around the launch), algorithmic bytes and FLOPs
+ * (per raster step, the graph decoder's accounting: weights + A rows + outputs once per GEMM, rANS inputs and
+ * outputs; times teams x Hb x Wb) and whether it ran with plain hand-off stores (1) or write-through ones (0). */
+int lbc_team_stats(const lbc_model *m, double *launch_ms, double *bytes, double *flops, int *plain);
 
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder

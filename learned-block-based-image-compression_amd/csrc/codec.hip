@@ -184,6 +184,9 @@ struct lbc_model {
     std::vector<long long> team_key;
     TeamArgs team_args{};
     std::vector<unsigned long long> team_ts_host;
+    int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
+    double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
+    double team_launch_bytes = 0, team_launch_flops = 0;
 };
 
 namespace {
@@ -1381,7 +1384,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
         if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned)))) return rc;
-        if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 64 * sizeof(unsigned long long)))) return rc;
+        if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
         TeamArgs& a = m0->team_args;
         a = TeamArgs{};
         a.gemm = m0->team_prog.as<GemmArgs>();
@@ -1394,6 +1397,34 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.Hb = Hb;
         a.Wb = Wb;
         a.sync = m0->team_sync.as<unsigned>();
+        // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices
+        // that end before it run beside the rANS decode when every workgroup takes the fast path for it
+        a.split_op = -1;
+        a.split_wy = 0;
+        for (int i = 0; i + 1 < (int)ops.size(); ++i) {
+            if (ops[i] != -1 || ops[i + 1] < 0 || getenv("LBIC_TEAM_NOSPLIT")) continue;
+            const GemmArgs& d = gem[ops[i + 1]];
+            const Seg& last = d.seg[d.nseg - 1];
+            if (last.kind != SEG_DENSE || last.base != ms[0]->lane[0].yq.as<float>() || !team_fast_path(d, S)) continue;
+            const int nkb = d.K >> 4, kby = last.k0 >> 4;
+            int wy = 0;
+            while (wy < KSPLIT && (wy + 1) * nkb / KSPLIT <= kby) ++wy;
+            if (wy >= 1 && wy <= KSPLIT - 1) {
+                a.split_op = i + 1;
+                a.split_wy = wy;
+            }
+        }
+        // algorithmic work of one raster step (the graph decoder's accounting, gemm(): weights + A rows + outputs
+        // [+ the GDN input] once per GEMM; rANS: indexes and means in, y_qnt out, the step's stream words)
+        double sb = 0, sf = 0;
+        for (int gi = 0; gi < NG; ++gi) {
+            const GemmArgs& d = gem[(size_t)1 * NG + gi];     // team 0, inner column class
+            sb += 4.0 * ((double)d.K * d.N + (double)d.M * d.K + (double)d.M * d.N * (d.square_a ? 2 : 1));
+            sf += 2.0 * d.M * d.K * d.N;
+        }
+        sb += 12.0 * n_img * m0->M;
+        m0->team_step_bytes = sb;
+        m0->team_step_flops = sf;
         m0->team_key = key;
     }
     TeamArgs a = m0->team_args;
@@ -1408,25 +1439,51 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s)))
             return rc;
     }
-    HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));
-    if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 64 * sizeof(unsigned long long), s));
-    HIPCHK(hipEventRecord(m0->ev[2], s));
-    if ((rc = launch_dec_team(a, s))) return rc;
-    HIPCHK(hipEventRecord(m0->ev[3], s));
+    // plain hand-off stores unless LBIC_TEAM_SC1=1; a launch that finds a team spread over XCDs stops before its
+    // first operation (failure word 2, nothing decoded yet) and is rerun with write-through hand-offs
+    const char* sc1e = getenv("LBIC_TEAM_SC1");
+    a.plain = sc1e && atoi(sc1e) ? 0 : 1;
+    unsigned fail = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));
+        if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 256 * sizeof(unsigned long long), s));
+        HIPCHK(hipEventRecord(m0->ev[2], s));
+        if ((rc = launch_dec_team(a, s))) return rc;
+        HIPCHK(hipEventRecord(m0->ev[3], s));
+        HIPCHK(hipMemcpyAsync(&fail, m0->team_sync.as<unsigned>() + T * 32, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (fail != 2 || !a.plain) break;
+        a.plain = 0;
+        m0->team_fallbacks += 1;
+    }
+    m0->team_plain_last = a.plain;
+    m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
+    m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
     m0->dec_timed = true;
     for (int t = 0; t < T; ++t)
         if ((rc = launch_copy_interior(ms[t]->zpad.as<float>(), zhat_devs[t], n_img, Hb, Wb, ms[t]->Cx, s))) return rc;
-    unsigned fail = 0;
-    HIPCHK(hipMemcpyAsync(&fail, m0->team_sync.as<unsigned>() + T * 32, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     if (a.ts) {
-        m0->team_ts_host.assign((size_t)T * 64, 0ull);
-        HIPCHK(hipMemcpyAsync(m0->team_ts_host.data(), m0->team_ts.p, (size_t)T * 64 * sizeof(unsigned long long),
+        m0->team_ts_host.assign((size_t)T * 256, 0ull);
+        HIPCHK(hipMemcpyAsync(m0->team_ts_host.data(), m0->team_ts.p, (size_t)T * 256 * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     if (fail) return set_error(LBC_E_HIP, "team decoder: a workgroup gave up waiting at a barrier (grid not resident?)");
+    if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
+        fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d\n", T, S, a.plain, m0->team_fallbacks);
     for (int t = 0; t < T; ++t)
         if ((rc = check_status(ms[t], (size_t)n_img, s))) return rc;
+    return LBC_OK;
+}
+
+int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double* flops, int* plain) {
+    if (!m || !launch_ms || !bytes || !flops || !plain) return set_error(LBC_E_ARG, "null argument");
+    float ms = 0.f;
+    if (m->dec_timed && m->ev[2]) HIPCHK(hipEventElapsedTime(&ms, m->ev[2], m->ev[3]));
+    *launch_ms = ms;
+    *bytes = m->team_launch_bytes;
+    *flops = m->team_launch_flops;
+    *plain = m->team_plain_last;
     return LBC_OK;
 }
 

@@ -113,12 +113,23 @@ struct TeamArgs {
     const RansArgs* rans;    // [T] (sparse decoder, one stream per image)
     int opk[TEAM_MAXOPS];    // the step: >= 0 a GEMM index, -1 the rANS decode
     int nops, NG, T, S, Hb, Wb;
-    unsigned* sync;          // [T][32] arrival counters (one 128-byte line each), then the failure word at [T * 32];
-                             // zeroed before every launch
+    unsigned* sync;          // [T][32]: per team [0] arrival counter, [1] XCD census (one 128-byte line each), then
+                             // [T * 32] the failure word (1 timeout, 2 a team spans XCDs) and [T * 32 + 1] the
+                             // census barrier; zeroed before every launch
+    int plain;               // 1: plain hand-off stores (needs every team on one XCD: checked in-kernel)
+    int split_op, split_wy;  // split_op >= 0: the GEMM after the rANS decode; its K slices w < split_wy (no y_qnt)
+                             // run beside the rANS decode, the rest after it
     unsigned long long tmo;  // s_memrealtime ticks (100 MHz) one barrier waits before the launch gives up
-    unsigned long long* ts;  // optional [T][64]: s_memrealtime after every barrier of raster step (sv, sh)
+    unsigned long long* ts;  // optional [T][256]: s_memrealtime after every barrier of raster step (sv, sh), then
+                             // [64 + 8 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
     int sv, sh;
 };
+// the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
+inline bool team_fast_path(const GemmArgs& g, int S) {
+    const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
+    const int ni = (items + S - 1) / S;
+    return S % MT == 0 && L >= 4 && L <= 9 && ni <= (L <= 7 ? 5 : 4);
+}
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
 int launch_dec_team(const TeamArgs& a, hipStream_t s);

@@ -15,290 +15,9 @@
 // and are summed in slice order.  The per-element arithmetic is therefore the same for every (BM, BN,
 // NW), which is what keeps the encoder's wavefront steps and the decoder's raster steps bit-identical
 // (the rANS decoder needs exactly the encoder's scale indexes).
-#include "kernels.h"
-
-#include <cmath>
-#include <string>
-
-#include "lbic_internal.h"
+#include "kernels_dev.h"
 
 namespace lbic {
-
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-// Kernel arguments are read with scalar loads through the scalar cache.  hipcc fetches the large argument
-// blocks field by field at first use, in several dependent rounds (a branch on one argument, then the loads
-// it guards, then a wait...), each an L2 round trip.  One asm statement touching every 64-byte line of the
-// block up front turns that into one round trip: the later, compiler-placed loads hit the scalar cache.
-// (Scalar LOADS only: nothing is written through the scalar cache.)
-template <int NLINES>
-__device__ __forceinline__ void warm_kernargs() {
-    static_assert(NLINES >= 1 && NLINES <= 10, "kernarg lines");
-    const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
-    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9;
-    if constexpr (NLINES <= 3) {
-        asm volatile("s_load_dword %0, %3, 0x0\n\ts_load_dword %1, %3, 0x40\n\ts_load_dword %2, %3, 0x80\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=s"(d0), "=s"(d1), "=s"(d2) : "s"(kp) : "memory");
-    } else {
-        asm volatile("s_load_dword %0, %10, 0x0\n\ts_load_dword %1, %10, 0x40\n\ts_load_dword %2, %10, 0x80\n\t"
-                     "s_load_dword %3, %10, 0xc0\n\ts_load_dword %4, %10, 0x100\n\ts_load_dword %5, %10, 0x140\n\t"
-                     "s_load_dword %6, %10, 0x180\n\ts_load_dword %7, %10, 0x1c0\n\ts_load_dword %8, %10, 0x200\n\t"
-                     "s_load_dword %9, %10, 0x230\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(d0), "=s"(d1), "=s"(d2), "=s"(d3), "=s"(d4), "=s"(d5), "=s"(d6), "=s"(d7), "=s"(d8), "=s"(d9)
-                     : "s"(kp) : "memory");
-    }
-}
-static_assert(sizeof(GemmArgs) <= 0x240 && sizeof(GemmArgs) > 0x230, "warm_kernargs<10> covers GemmArgs");
-static_assert(sizeof(RansArgs) <= 0xC0, "warm_kernargs<3> covers RansArgs");
-
-static int launch_status(const char* what) {
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, std::string(what) + " launch failed: " + hipGetErrorString(e));
-}
-
-// Launch-span stamps for sampled launches (bench.py's per-kernel roofline).  HIP events cannot be
-// recorded inside a captured graph on ROCm 7.2, so the kernels stamp themselves on the constant 100 MHz
-// clock: per XCD (the counters of different XCDs need not agree) the earliest workgroup start and the
-// latest workgroup end, slot = 8 x {max(~start), max(end)}; slots are zeroed at every graph replay.
-__device__ __forceinline__ int xcc_id() {
-    int v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return v & 7;
-}
-__device__ __forceinline__ void stamp_start(unsigned long long* ts) {
-    if (ts && threadIdx.x == 0)
-        atomicMax(ts + 2 * xcc_id(), ~0ull - (unsigned long long)__builtin_amdgcn_s_memrealtime());
-}
-__device__ __forceinline__ void stamp_end(unsigned long long* ts) {
-    if (ts) {
-        __syncthreads();
-        if (threadIdx.x == 0) atomicMax(ts + 2 * xcc_id() + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
-}
-
-#ifdef LBIC_PHASE_STAMPS
-// diagnostic build only (csrc/microbench.hip): per-workgroup s_memtime at phase boundaries
-__device__ unsigned long long* g_phase;
-// (launch slot = g.ctr_stride, which the microbenchmark's dense-only launches do not otherwise use)
-#define PHASE(i)                                                                                  \
-    do {                                                                                          \
-        const long ph_ = ((long)g.ctr_stride * 4096 + blockIdx.y * gridDim.x + blockIdx.x) * 8;   \
-        if (threadIdx.x == 0) g_phase[ph_ + (i)] = __builtin_amdgcn_s_memtime();                   \
-        if (threadIdx.x == 0 && (i) == 0) g_phase[ph_ + 7] = xcc_id();                            \
-    } while (0)
-#else
-#define PHASE(i) do {} while (0)
-#endif
-
-#ifdef LBIC_PHASE_DIAG
-// diagnostic library build only (make diag -> liblbic_diag.so, LBIC_LIB_VARIANT=diag): sampled k_gemm_s launches
-// record, per phase boundary i = 1..4, the max and the sum over workgroups of (s_memtime at i - at kernel start)
-// in slot words 16 + i / 24 + i, and the workgroup count in word 31 (lbc_profile_end prints them)
-#define DPH(i)                                                                                    \
-    do {                                                                                          \
-        if (g.ts && threadIdx.x == 0) {                                                           \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
-            if ((i) == 0) dph0_ = t_;                                                             \
-            else {                                                                                \
-                atomicMax(g.ts + 16 + (i), t_ - dph0_);                                           \
-                atomicAdd(g.ts + 24 + (i), t_ - dph0_);                                           \
-                if ((i) == 4) atomicAdd(g.ts + 31, 1ull);                                         \
-            }                                                                                     \
-        }                                                                                         \
-    } while (0)
-#else
-#define DPH(i) do {} while (0)
-#endif
-
-__device__ __forceinline__ int scale_index(float s, const float* table) {
-    // build_indexes (entropy_layers_cai.py:649-654): idx = 63 - #{k < 63 : max(s, .11) <= table[k]}
-    s = fmaxf(s, 0.11f);
-    int idx = 63;
-#pragma unroll 8
-    for (int k = 0; k < 63; ++k) idx -= (s <= table[k]) ? 1 : 0;
-    return idx;
-}
-
-__device__ __forceinline__ float std_cum(float x) {
-    // _standardized_cumulative (entropy_layers_cai.py:569-573)
-    return 0.5f * erfcf(-0.70710677f * x);
-}
-
-// Plain, or write-through (sc1) / L1-bypassing (sc1) global accesses: the team decoder (k_dec_team) hands every
-// value it writes to other workgroups of the same launch (cdna_hip_programming.md §6 Guideline 16, R1).
-template <typename T>
-using gptr = __attribute__((address_space(1))) T*;
-template <bool SC1, typename T>
-__device__ __forceinline__ void st(T* p, T v) {
-    if constexpr (SC1) __hip_atomic_store((gptr<T>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
-template <bool SC1, typename T>
-__device__ __forceinline__ T ld(const T* p) {
-    if constexpr (SC1) return __hip_atomic_load((gptr<T>)const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-
-// Block (img, v, h) of A-row block m: from the block list, or computed for a decoder raster step
-// (GemmArgs::raster: img = img0 + m, v = the graph's row counter, h fixed), which saves the kernel one
-// dependent global load before its first activation load.
-struct BlkSrc {
-    const int4* p;
-    int raster, img0, v, h;
-    __device__ __forceinline__ int4 at(int m) const { return raster ? make_int4(img0 + m, v, h, 0) : p[m]; }
-};
-
-// Output element (row, col) of a GEMM from its slice-ordered sum v: bias + the layer's epilogue.  Shared by
-// both GEMM kernels so that they compute bit-identical values.
-// bcol = bias[col]; xv = the GDN input x[row][col] (GDN / IGDN only), both loaded by the caller.
-template <bool SC1 = false>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const BlkSrc& blocks, float bcol,
-                                         float xv) {
-    switch (g.epi) {
-        case EPI_BIAS:
-            st<SC1>(g.out + (long)row * g.ldo + col, v + bcol);
-            break;
-        case EPI_LEAKY: {
-            const float t = v + bcol;
-            float o = t > 0.f ? t : t * 0.01f;
-            if (g.zero_oob) {    // row = block * P + position; position outside the frame -> 0
-                const int m = row / g.P, p = row - m * g.P;
-                int dy = 0, dx = 0;
-#pragma unroll
-                for (int q = 0; q < 5; ++q) {
-                    dy = p == q ? g.pos_dy[q] : dy;
-                    dx = p == q ? g.pos_dx[q] : dx;
-                }
-                const int4 b = blocks.at(m);
-                const int vv = b.y + dy, hh = b.z + dx;
-                if (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb) o = 0.f;
-            }
-            st<SC1>(g.out + (long)row * g.ldo + col, o);
-            break;
-        }
-        case EPI_LEAKY_L0: {   // row = block * P + position -> the layer-0 cache cell of that position
-            const float t = v + bcol;
-            float o = t > 0.f ? t : t * 0.01f;
-            const int m = row / g.P, p = row - m * g.P;
-            int dy = 0, dx = 0;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                dy = p == q ? g.pos_dy[q] : dy;
-                dx = p == q ? g.pos_dx[q] : dx;
-            }
-            const int4 b = blocks.at(m);
-            const int vv = b.y + dy, hh = b.z + dx;
-            if (g.zero_oob && (vv < 0 || vv >= g.geo.Hb || hh < 0 || hh >= g.geo.Wb)) o = 0.f;
-            st<SC1>(g.out + (((long)b.x * g.geo.Hp + vv + 2) * g.geo.Wp + hh + 2) * g.ldo + col, o);
-            break;
-        }
-        case EPI_GDN:
-        case EPI_IGDN: {
-            const float norm = v + bcol;
-            const float sq = __fsqrt_rn(norm);
-            st<SC1>(g.out + (long)row * g.ldo + col, g.epi == EPI_GDN ? xv * __fdiv_rn(1.0f, sq) : xv * sq);
-            break;
-        }
-        case EPI_QUANT: {
-            const float y = v + bcol;
-            const float scale = g.ksi[(long)row * g.ldk + col];
-            const float mean = g.ksi[(long)row * g.ldk + g.Mlat + col];
-            const float d = y - mean;
-            const int sym = (int)rintf(d);               // torch.round: half to even
-            const float yq = (float)sym + mean;
-            st<SC1>(g.out + (long)row * g.ldo + col, yq);
-            const int4 b = blocks.at(row);
-            const long pos = ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.Mlat + col;
-            st<SC1>(g.sym + pos, (int32_t)sym);
-            st<SC1>(g.idx + pos, (int32_t)(g.table ? scale_index(scale, g.table) : 0));   // no table: forward()/validation before update()
-            if (g.bits) {
-                const float av = fabsf(yq - mean), sb = fmaxf(scale, 0.11f);
-                const float lik = std_cum((0.5f - av) / sb) - std_cum((-0.5f - av) / sb);
-                st<SC1>(g.bits + pos, -log2f(fmaxf(lik, 1e-9f)));
-            }
-            break;
-        }
-        case EPI_CTXIDX: {
-            const float t = v + bcol;
-            st<SC1>(g.out + (long)row * g.ldo + col, t);
-            if (col < g.Mlat) st<SC1>(g.idx + (long)row * g.Mlat + col, (int32_t)scale_index(t, g.table));
-            break;
-        }
-        case EPI_SCATTER: {   // output row of block (img, v, h) -> out[img][v][h][col] (forward()'s xhat)
-            const int4 b = blocks.at(row);
-            st<SC1>(g.out + ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col, v + bcol);
-            break;
-        }
-        case EPI_CLAMPZ: {
-            const float t = fminf(fmaxf(v + bcol, -0.5f), 0.5f);
-            const int4 b = blocks.at(row);
-            st<SC1>(g.geo.zpad + ((long)(b.x * g.geo.Hp + b.y + 2) * g.geo.Wp + b.z + 2) * g.geo.Cx + col, t);
-            break;
-        }
-    }
-}
-
-// A / W fragments of one 16-wide k-block for this lane (operand maps: the packing comment in codec.hip)
-template <int MS, int NS>
-struct Frag {
-    f4 a[MS];
-    f4 w[NS];
-};
-
-constexpr int MAXSEG = 6;
-
-// Source addressing without branches in the k-loop: every lane precomputes, per segment t and row
-// subtile s, a 32-bit offset from that segment's base pointer; a k-block then selects its segment with
-// uniform compares (SALU) and the offset with v_cndmask, so the compiler never branches around a load (a
-// branch per load makes hipcc drain vmcnt(0) each time: cdna_hip_programming.md §5, "Three .s-level traps",
-// (c)).  Offsets count float4s (every row offset, tap offset and k-block start is a multiple of 4 floats:
-// widths and 3B^2 are padded to 16) and are unsigned: computed in 64 bits, they address 2^32 float4s (64 GB)
-// from a base, so a ganged decoder workspace of more than 2^31 floats stays in range at no cost per load.
-template <int MS>
-struct Rows {
-    unsigned off[MAXSEG][MS];
-};
-
-template <int MS, int NS>
-__device__ __forceinline__ void load_kb(const GemmArgs& g, int kb, int nb0, const Rows<MS>& R, int q4, int lane,
-                                        Frag<MS, NS>& f) {
-    const int k = kb << 4;
-    const float* base = g.seg[0].base;
-    int k0 = g.seg[0].k0;
-    unsigned o[MS];
-#pragma unroll
-    for (int s = 0; s < MS; ++s) o[s] = R.off[0][s];
-#pragma unroll
-    for (int t = 1; t < MAXSEG; ++t) {
-        const bool in = k >= g.seg[t].k0;     // wave-uniform (unused segments: k0 past K)
-        base = in ? g.seg[t].base : base;
-        k0 = in ? g.seg[t].k0 : k0;
-#pragma unroll
-        for (int s = 0; s < MS; ++s) o[s] = in ? R.off[t][s] : o[s];
-    }
-    const unsigned kk4 = (unsigned)(k - k0 + q4) >> 2;
-#pragma unroll
-    for (int s = 0; s < MS; ++s) f.a[s] = reinterpret_cast<const f4*>(base)[o[s] + kk4];
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-#pragma unroll
-    for (int j = 0; j < NS; ++j) f.w[j] = Wt[((long)kb * g.NB16 + nb0 + j) * 64];
-}
-
-template <int MS, int NS>
-__device__ __forceinline__ void mma_kb(const GemmArgs& g, Frag<MS, NS>& f, f4 (&acc)[MS][NS]) {
-    if (g.square_a) {
-#pragma unroll
-        for (int s = 0; s < MS; ++s) f.a[s] = f.a[s] * f.a[s];
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int s = 0; s < MS; ++s)
-#pragma unroll
-            for (int j = 0; j < NS; ++j)
-                acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[s][e], f.w[j][e], acc[s][j], 0, 0, 0);
-}
 
 // CH k-blocks per chunk: all their loads are issued together, and chunk c+1 is in flight while chunk c
 // is multiplied, so a slice of K costs about one memory round trip instead of one per k-block.
@@ -409,80 +128,6 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
     }
     PHASE(4);
     stamp_end(g.ts);
-}
-
-// Small-M GEMM (the decoder's per-step batch, M = n_img rows, and the wavefront's ramp steps): one
-// 16 x 16 output tile per workgroup, 8 waves = the 8 K slices, one slice per wave.  Latency-shaped:
-// every weight and activation fragment of a slice is requested before the first MFMA (the weights
-// first: they need nothing but the kernel arguments), and bias / GDN input of the epilogue at the start
-// too, so a launch costs about one memory round trip plus the slice's dependent MFMA chain.  The slice
-// length L (k-blocks) is dispatched to a fully unrolled body, so no load sits behind a branch.  Slices,
-// chain order and the slice-ordered sum are those of k_gemm: results are bit-identical to it.
-typedef const float __attribute__((address_space(1)))* gfloat_p;   // global (not flat) loads
-
-struct SRow {            // per-lane A addressing of every segment, computed once per launch
-    gfloat_p base[MAXSEG];
-    int k0[MAXSEG];
-    unsigned off[MAXSEG];   // float4 offset of this lane's row in segment t, minus k0 (plus q4), mod 2^32 (Rows)
-};
-
-// this lane's A row: the row, its block (img, v, h) when a segment or the epilogue needs it, and its
-// context position; the block load is issued here and waited for only in small_offsets
-struct SBlk {
-    int r, dy, dx;
-    int4 b;
-};
-
-template <bool RASTER>
-__device__ __forceinline__ SBlk small_blk(const GemmArgs& g, int m0, int lane, const BlkSrc& blocks) {
-    SBlk s;
-    s.r = min(m0 + (lane & 15), g.M - 1);
-    int m = s.r;
-    s.dy = s.dx = 0;
-    if (g.P > 1) {
-        m = s.r / g.P;
-        const int p = s.r - m * g.P;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {         // static indices only (a per-lane index would copy g to scratch)
-            s.dy = p == q ? g.pos_dy[q] : s.dy;
-            s.dx = p == q ? g.pos_dx[q] : s.dx;
-        }
-    }
-    if constexpr (RASTER) s.b = make_int4(blocks.img0 + m, blocks.v, blocks.h, 0);
-    else s.b = blocks.p[m];   // unconditional (a branch here costs a full vmcnt drain); unused by dense-only GEMMs
-    return s;
-}
-
-__device__ __forceinline__ void small_offsets(const GemmArgs& g, const SBlk& k, int lane, SRow& s) {
-    const int4 b = k.b;
-    const long cell = ((long)b.x * g.geo.Hp + b.y + 2 + k.dy) * g.geo.Wp + b.z + 2 + k.dx;
-    const long xrow = (((long)b.x * g.geo.Hb + b.y) * g.geo.Wb + b.z) * g.geo.Cx;
-    const int q4 = (lane >> 4) * 4;
-#pragma unroll
-    for (int t = 0; t < MAXSEG; ++t) {
-        const Seg& sg = g.seg[t];
-        s.base[t] = (gfloat_p)sg.base;
-        s.k0[t] = sg.k0;
-        // opaque from here on: the per-k-block selects pick values, not kernel-argument addresses
-        // (a selected address would become one dependent scalar load per k-block)
-        asm volatile("" : "+s"(s.base[t]), "+s"(s.k0[t]));
-        const long o = (long)k.r * sg.ld + sg.zs * cell + (sg.xs ? xrow : 0l) + sg.tap - sg.k0 + q4;
-        s.off[t] = (unsigned)(o >> 2);     // may wrap below zero: + k / 4 in small_a lands in range
-    }
-}
-
-// A fragment of k-block kb (elements kb*16 + q4 .. +3 of this lane's row)
-__device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
-    const int k = kb << 4;
-    gfloat_p base = rw.base[0];
-    unsigned o = rw.off[0];
-#pragma unroll
-    for (int t = 1; t < MAXSEG; ++t) {
-        const bool in = k >= rw.k0[t];     // wave-uniform; unused segments have k0 past K
-        base = in ? rw.base[t] : base;
-        o = in ? rw.off[t] : o;
-    }
-    return reinterpret_cast<const f4 __attribute__((address_space(1)))*>(base)[o + (unsigned)(k >> 2)];
 }
 
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
@@ -740,37 +385,9 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
 //   * the block's stream words are staged in LDS with the tables; renormalisation takes the next word
 //     from there, requested as soon as the previous one is consumed.
 // Output: y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
-#ifndef LBIC_RANS_WPB
-#define LBIC_RANS_WPB 4   // one wave per SIMD: a lone wave issues its latency-bound chain ~13 % faster than two
-#endif
-constexpr int RANS_WPB = LBIC_RANS_WPB;   // waves (streams) per workgroup
-constexpr int RANS_MAXLAT = 256;          // Mlat <= 4 * 64
-constexpr int RANS_WIN = 512;             // stream words staged in LDS per wave and launch (>= 52/32 * MAXLAT)
-constexpr int RANS_FILL = 8192 / (RANS_WPB * 64);   // 16-byte table loads per thread in flight (128 KB per pass)
-
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-__device__ __forceinline__ int rdlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
-__device__ __forceinline__ unsigned long long uni64(unsigned long long v) {   // keep a uniform value in SGPRs
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return ((unsigned long long)hi << 32) | lo;
-}
-
 // Called by every wave of the workgroup (rows past a.rows only help fill the LDS tables): the wave's
 // stream state and indexes are requested first, the workgroup then copies the tables into LDS while those
 // loads are in flight.
-#ifdef LBIC_RANS_STAMPS
-__device__ unsigned long long* g_rdbg;   // diagnostic build (rans_bench): per wave s_memtime at 4 points
-#define RSTAMP(k)                                                                                    \
-    do {                                                                                             \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                  \
-        if (lane == 0 && row_in < a.rows) g_rdbg[row_in * 4 + (k)] = t_;                             \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-    } while (0)
-#else
-#define RSTAMP(k) do {} while (0)
-#endif
 __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int row_in, int lane) {
     RSTAMP(0);
     const bool valid = row_in < a.rows;
@@ -941,202 +558,6 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     RSTAMP(3);
 }
 
-// Sparse variant (low rates: almost every symbol is the most probable one, value 0).  No table image in LDS:
-// per symbol ONE compare of cum against the centre interval [lo, lo + freq) of the symbol's table (tmeta row
-// 5, gathered into a lane-per-symbol register in the prologue) decides; a hit costs the 64-bit state update
-// and nothing else.  A miss compares against the intervals of values -1 and +1 (rows 6 and 7, SALU only), then
-// runs the two-level search of rans_row on the table image in global memory (the 70 KB image stays L2-resident:
-// every launch of every decoder reads it).  The prologue therefore needs only
-// the stream state, the block's indexes and the stream words -- no 70 KB LDS fill and no workgroup barrier
-// for it -- and each wave is independent.  Bit-identical to rans_row (same coder, same tables).
-// SC1: inside k_dec_team (indexes and means from the context net's workgroups, y_qnt to the decoder's)
-template <bool SC1 = false>
-__device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane) {
-    RSTAMP(0);
-    const bool valid = row_in < a.rows;
-    const int row = valid ? row_in : a.rows - 1;
-    int img = row;
-    if (a.streams_per_img > 1) {
-        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
-        const int4 blk = blocks[row];
-        img = blk.x * a.streams_per_img + blk.y;
-    }
-    img = __builtin_amdgcn_readfirstlane(img);
-    const int Mlat = a.Mlat;
-    const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
-    const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane], t_lf = a.tmeta[320 + lane];
-    const int t_lfm = a.tmeta[384 + lane], t_lfp = a.tmeta[448 + lane];
-    const unsigned long long x_in = a.state_x[img];
-    const int p_in = a.state_ptr[img];
-    const long long wb = a.word_base[img];
-    const int nw_in = a.word_count[img];
-    int ti[4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) ti[kb] = ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1)) & 63;
-    unsigned long long x = uni64(x_in);
-    int p = __builtin_amdgcn_readfirstlane(p_in);
-    const uint32_t* w = a.words + wb;
-    const int nw = __builtin_amdgcn_readfirstlane(nw_in);
-    const int p0 = p;
-    {
-        uint32_t wv[RANS_WIN / 64];
-#pragma unroll
-        for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
-#pragma unroll
-        for (int k = 0; k < RANS_WIN / 64; ++k) lwin[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
-    }
-    // lane i of chunk kb = symbol 64 kb + i: its centre interval (lo, freq), table metadata and offset
-    int lov[4], frv[4], ivm[4], ivp[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int sel = ti[kb] << 2;
-        const int lf = __builtin_amdgcn_ds_bpermute(sel, t_lf);
-        lov[kb] = lf & 0xffff;
-        frv[kb] = (int)((uint32_t)lf >> 16);
-        ivm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lfm);
-        ivp[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lfp);
-        sfb[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
-        sS[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
-        slm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
-        sca[kb] = __builtin_amdgcn_ds_bpermute(sel, t_ca);
-        moff[kb] = __builtin_amdgcn_ds_bpermute(sel, t_off);
-        symv[kb] = -moff[kb];            // the centre symbol's index (value 0)
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the window is in LDS (this wave's own writes)
-    __builtin_amdgcn_wave_barrier();
-    if (!valid) return;
-    RSTAMP(1);
-    int bad = 0;
-    int q0 = 0;
-    uint32_t wbuf = lwin[lane];
-    uint32_t wn = rdlane(wbuf, 0);
-    auto renorm_slow = [&]() {           // x < 2^31: shift in the next stream word
-        x = (x << 32) | wn;
-        ++p;
-        if (p - p0 - q0 >= 64) {
-            q0 = min(q0 + 64, RANS_WIN - 64);
-            wbuf = lwin[q0 + lane];
-        }
-        wn = rdlane(wbuf, min(p - p0 - q0, 63));
-    };
-    auto renorm = [&]() {
-        uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);   // 0 <=> x < RANS64_L = 2^31
-        asm("" : "+s"(t));
-        if (t == 0) renorm_slow();
-        x = uni64(x);
-    };
-    const uint16_t* img16 = a.cdf16;
-    const int lane2 = lane * 2;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int cnt_i = __builtin_amdgcn_readfirstlane(min(64, Mlat - kb * 64));
-        if (cnt_i <= 0) break;
-        // one most-probable symbol: a compare, the 64-bit state update, a (rare) renormalisation
-        auto fast = [&](uint32_t lo, uint32_t fr) -> bool {
-            const uint32_t d = ((uint32_t)x & 0xffffu) - lo;
-            if (d >= fr) return false;
-            x = (unsigned long long)fr * (x >> 16) + d;
-            const uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);
-            if (__builtin_expect(t == 0, 0)) renorm_slow();
-            return true;
-        };
-        // one centre step of the state, no test: the caller checks d < fr and the renormalisation bound afterwards
-        auto step = [](unsigned long long xv, uint32_t lo, uint32_t fr, uint32_t& bad) -> unsigned long long {
-            const uint32_t d = ((uint32_t)xv & 0xffffu) - lo;
-            bad |= d >= fr ? 1u : 0u;
-            const unsigned long long xn = (unsigned long long)fr * (xv >> 16) + d;
-            bad |= ((uint32_t)(xn >> 32) | ((uint32_t)xn >> 31)) == 0u ? 1u : 0u;   // x < 2^31: renormalise
-            return xn;
-        };
-        int ii = 0;
-        while (ii < cnt_i) {
-            // runs of most-probable symbols, 4 per iteration, speculatively: the 8 interval reads (v_readlane,
-            // independent of the state) first, then 4 state updates with no branch between them, one test at the end
-            // (a symbol outside its centre interval or a renormalisation anywhere in the four); on a hit the four are
-            // committed, otherwise the state is restored and the careful loop below decodes them one by one
-            while (ii + 4 <= cnt_i) {
-                const uint32_t l0 = rdlane((uint32_t)lov[kb], ii), f0 = rdlane((uint32_t)frv[kb], ii);
-                const uint32_t l1 = rdlane((uint32_t)lov[kb], ii + 1), f1 = rdlane((uint32_t)frv[kb], ii + 1);
-                const uint32_t l2 = rdlane((uint32_t)lov[kb], ii + 2), f2 = rdlane((uint32_t)frv[kb], ii + 2);
-                const uint32_t l3 = rdlane((uint32_t)lov[kb], ii + 3), f3 = rdlane((uint32_t)frv[kb], ii + 3);
-                uint32_t bad = 0;
-                unsigned long long xv = step(x, l0, f0, bad);
-                xv = step(xv, l1, f1, bad);
-                xv = step(xv, l2, f2, bad);
-                xv = step(xv, l3, f3, bad);
-                if (__builtin_amdgcn_readfirstlane(bad)) break;
-                x = uni64(xv);
-                ii += 4;
-            }
-            while (ii < cnt_i && fast(rdlane((uint32_t)lov[kb], ii), rdlane((uint32_t)frv[kb], ii))) ++ii;
-            if (ii >= cnt_i) break;
-            const uint32_t cum = (uint32_t)x & 0xffffu;
-            // value -1 or +1 (most of the misses): two more interval compares, no memory access
-            {
-                const uint32_t im = rdlane((uint32_t)ivm[kb], ii), ip = rdlane((uint32_t)ivp[kb], ii);
-                const uint32_t dm = cum - (im & 0xffffu), dp = cum - (ip & 0xffffu);
-                const bool hm = dm < (im >> 16), hp = dp < (ip >> 16);
-                if (hm || hp) {
-                    const uint32_t fr = hm ? im >> 16 : ip >> 16, d = hm ? dm : dp;
-                    x = (unsigned long long)fr * (x >> 16) + d;
-                    renorm();
-                    symv[kb] = lane == ii ? symv[kb] + (hm ? -1 : 1) : symv[kb];
-                    ++ii;
-                    continue;
-                }
-            }
-            // another symbol: the two-level search of rans_row on the table image in global memory
-            const int fb = rdlane_i(sfb[kb], ii), S = rdlane_i(sS[kb], ii);
-            const int lm2 = rdlane_i(slm[kb], ii), ca = rdlane_i(sca[kb], ii);
-            const uint32_t cv = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + ca + lane2);
-            const int j = __popcll(__ballot(cv < cum));
-            const int sbb = j * S;
-            const uint32_t fine = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + fb + sbb + lane2);
-            const int kk = __popcll(__ballot(fine < cum) | 1ull) - 1;
-            const int sidx = (sbb >> 1) + kk;
-            const uint32_t start = (rdlane(fine, kk) + 1u) & 0xffffu;
-            const uint32_t nxt = rdlane(fine, kk + 1) + 1u;
-            x = (unsigned long long)(nxt - start) * (x >> 16) + (cum - start);
-            renorm();
-            int v = sidx;
-            if (__builtin_expect(sidx == lm2, 0)) {   // escape: value coded in 4-bit bypass chunks
-                auto get_bits = [&]() -> uint32_t {
-                    const uint32_t b = (uint32_t)(x & 15u);
-                    x >>= 4;
-                    renorm();
-                    return b;
-                };
-                uint32_t cc = get_bits(), nb = cc;
-                while (cc == 15u && nb <= 8) { cc = get_bits(); nb += cc; }
-                if (nb > 8) { bad |= 4; nb = 0; }
-                uint32_t raw = 0;
-                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits() << (jj * 4);
-                v = (int)(raw >> 1);
-                v = (raw & 1) ? -v - 1 : v + lm2;
-            }
-            symv[kb] = lane == ii ? v : symv[kb];
-            ++ii;
-        }
-    }
-    RSTAMP(2);
-    bad |= p > nw;
-    bad |= (p - p0 > RANS_WIN) ? 8 : 0;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int i = kb * 64 + lane;
-        if (i < Mlat) {
-            if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
-            else st<SC1>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + ld<SC1>(a.ksi + (long)row * a.ldk + Mlat + i));
-        }
-    }
-    if (lane == 0) {
-        a.state_x[img] = x;
-        a.state_ptr[img] = p;
-        if (bad) a.status[img] = bad;
-    }
-    RSTAMP(3);
-}
-
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];
     warm_kernargs<3>();
@@ -1175,280 +596,6 @@ int launch_rans_decode(const RansArgs& a, hipStream_t s) {
     const int wpb = a.rows < RANS_WPB ? a.rows : RANS_WPB;
     hipLaunchKernelGGL(k_rans_decode, dim3((a.rows + RANS_WPB - 1) / RANS_WPB), dim3(wpb * 64), lds, s, a);
     return launch_status("k_rans_decode");
-}
-
-// ----------------------------------------------------------------------------------------- team decoder
-// k_dec_team: the reference-format raster decodes of T batches in ONE persistent launch.  Team t = the S
-// workgroups with blockIdx % T == t decodes batch t (with T = 8 a team's workgroups share one XCD under the
-// observed round-robin placement: speed only, nothing depends on it).  A team runs its batch's raster steps with
-// the operations the graph decoder launches -- context net x 4, rANS, decoder x 7, recorded by the host as
-// prepared GemmArgs / RansArgs -- and a team barrier between operations instead of a kernel boundary: a raster
-// step of 12 dependent launches pays 12 barriers (one agent-scope arrival per workgroup, one polling lane) in
-// place of 12 launch boundaries, and T chains run side by side in one launch instead of one per hardware queue
-// (at most four overlap: DESIGN.md §5).
-// Hand-offs follow cdna_hip_programming.md §6 Guideline 16, R1: every value a workgroup writes for the others
-// (activations, scale indexes, y_qnt, the reconstruction and the layer-0 cache) is stored sc1 (write-through),
-// every storing wave drains (vmcnt(0)) before its workgroup's single arrival, and every load of such a value is an
-// sc1 load (buffer_load ... sc1 for the GEMM A operand, global sc1 loads for the GDN inputs and the rANS inputs);
-// weights, biases and the tables are read-only.  Every spin is bounded (TeamArgs::tmo): a workgroup that gives up
-// sets the failure word, which every other waiter reads, so the whole grid drains and the host reports an error.
-// GEMM arithmetic per output element is k_gemm_s's (KSPLIT slices, the same MFMA chains, the slice-ordered sum,
-// the shared epilogue): results are bit-identical to the graph decoder's.
-
-// A fragment of k-block kb through an sc1 (L1-bypassing) buffer load; byte offsets < 4 GB (host-checked)
-__device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
-    const int k = kb << 4;
-    gfloat_p base = rw.base[0];
-    unsigned o = rw.off[0];
-#pragma unroll
-    for (int t = 1; t < MAXSEG; ++t) {
-        const bool in = k >= rw.k0[t];
-        base = in ? rw.base[t] : base;
-        o = in ? rw.off[t] : o;
-    }
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, -1, 0x00020000);
-    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (o + (unsigned)(k >> 2)) << 4, 0, 16));
-}
-
-// one GEMM of the step, this workgroup's share: output tiles (row tile mt, column tile nt) = item i = nt * MT + mt,
-// items rank, rank + S, ...; the weight fragments of the next item are requested before the current item's chain
-template <int L, bool EXACT>
-__device__ __forceinline__ void team_gemm(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
-    constexpr int LL = EXACT ? L : L + 1;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nkb = g.K >> 4;
-    const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
-    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
-    if (rank >= items) return;
-    const BlkSrc blocks{nullptr, 1, 0, v, h};
-    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
-    f4 a[LL], w0[LL], w1[LL];
-    float b0 = 0.f, x0 = 0.f, b1 = 0.f, x1 = 0.f;
-    int amt = -1, buf = 0;
-    auto issue = [&](int it, f4 (&w)[LL], float& bb, float& xx) {
-        const int mt = it % MT, nt = it / MT;
-        const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
-        bb = g.bias[ecol];
-        xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
-#pragma unroll
-        for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-    };
-    auto load_a = [&](int mt) {
-        const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
-        SRow rw;
-        small_offsets(g, bk, lane, rw);
-#pragma unroll
-        for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
-        amt = mt;
-    };
-    auto run = [&](int it, f4 (&w)[LL], float bb, float xx) {
-        const int mt = it % MT, nt = it / MT;
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < LL; ++c) {
-            f4 av = a[c];
-            if (g.square_a) av = av * av;
-            f4 t = acc;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-            acc = c < n ? t : acc;
-        }
-        float* rb = red + buf * (KSPLIT * 256);
-        buf ^= 1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only: the next item's weight loads stay in flight
-        __builtin_amdgcn_s_barrier();
-        if (threadIdx.x < 256) {
-            const int e = threadIdx.x;
-            float vv = rb[e];
-#pragma unroll
-            for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
-            const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
-            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx);
-        }
-    };
-    int it = rank;
-    issue(it, w0, b0, x0);
-    load_a(it % MT);
-    while (true) {           // two named weight buffers, statically indexed
-        int nx = it + S;
-        if (nx < items) issue(nx, w1, b1, x1);
-        run(it, w0, b0, x0);
-        if (nx >= items) break;
-        if (nx % MT != amt) load_a(nx % MT);
-        it = nx;
-        nx = it + S;
-        if (nx < items) issue(nx, w0, b0, x0);
-        run(it, w1, b1, x1);
-        if (nx >= items) break;
-        if (nx % MT != amt) load_a(nx % MT);
-        it = nx;
-    }
-}
-
-// K beyond 8 x 12 k-blocks: each item's slice in chunks of 12 k-blocks, A and weights per chunk, no prefetch
-__device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
-    constexpr int CH = 12;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nkb = g.K >> 4;
-    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
-    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
-    const BlkSrc blocks{nullptr, 1, 0, v, h};
-    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
-    int buf = 0;
-    for (int it = rank; it < items; it += S) {
-        const int mt = it % MT, nt = it / MT;
-        const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
-        const float bb = g.bias[ecol];
-        const float xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
-        const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
-        SRow rw;
-        small_offsets(g, bk, lane, rw);
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        for (int c0 = kb0; c0 < kb1; c0 += CH) {
-            const int cn = min(CH, kb1 - c0);
-            f4 a[CH], w[CH];
-#pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                const int kb = min(c0 + c, nkb - 1);
-                w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
-                a[c] = small_a_sc1(rw, kb);
-            }
-#pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                f4 av = a[c];
-                if (g.square_a) av = av * av;
-                f4 t = acc;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-                acc = c < cn ? t : acc;
-            }
-        }
-        float* rb = red + buf * (KSPLIT * 256);
-        buf ^= 1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-        if (threadIdx.x < 256) {
-            const int e = threadIdx.x;
-            float vv = rb[e];
-#pragma unroll
-            for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
-            const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
-            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx);
-        }
-    }
-}
-
-__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red) {
-    const int nkb = g.K >> 4;
-    const int L = nkb / KSPLIT;
-    const bool exact = (nkb % KSPLIT) == 0;
-    switch (L) {
-#define LBIC_T(L_)                                                                                 \
-    case L_:                                                                                       \
-        if (exact) team_gemm<L_, true>(g, v, h, rank, S, red);                                     \
-        else team_gemm<L_, false>(g, v, h, rank, S, red);                                          \
-        break;
-        case 0: team_gemm<0, false>(g, v, h, rank, S, red); break;
-        LBIC_T(1) LBIC_T(2) LBIC_T(3) LBIC_T(4) LBIC_T(5) LBIC_T(6)
-        LBIC_T(7) LBIC_T(8) LBIC_T(9) LBIC_T(10) LBIC_T(11)
-#undef LBIC_T
-        default: team_gemm_long(g, v, h, rank, S, red);
-    }
-}
-
-// team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
-// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else)
-__device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
-                                          int* sflag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int f = 0;
-        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                f = 1;
-                break;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-                __hip_atomic_store((gptr<unsigned>)fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                f = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        *sflag = f;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
-    return *sflag == 0;
-}
-
-__global__ __launch_bounds__(512) void k_dec_team(const TeamArgs ta) {
-    __shared__ __attribute__((aligned(16))) float red[2 * KSPLIT * 256];
-    __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
-    __shared__ int sflag;
-    const int T = ta.T, S = ta.S;
-    const int team = blockIdx.x % T, rank = blockIdx.x / T;
-    if (rank >= S) return;
-    unsigned* ctr = ta.sync + team * 32;
-    unsigned* fail = ta.sync + T * 32;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // the recorded operations are read-only for the launch: constant address space, so their fields come in by
-    // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
-    typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
-    typedef const __attribute__((address_space(4))) RansArgs* crans_p;
-    const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
-    const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
-    unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 64 : nullptr;
-    if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
-    unsigned target = 0;
-    for (int v = 0; v < ta.Hb; ++v) {
-        for (int h = 0; h < ta.Wb; ++h) {
-            const int cls = h == 0 ? 0 : h == ta.Wb - 1 ? 2 : 1;
-            const bool samp = ts && v == ta.sv && h == ta.sh;
-            for (int op = 0; op < ta.nops; ++op) {
-                const int k = ta.opk[op];
-                if (k >= 0) {
-                    team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + k), v, h, rank, S, red);
-                } else if (wave == 0) {
-                    for (int r = rank; r < R.rows; r += S) rans_row_sparse<true>(R, lwin, r, lane);
-                }
-                target += S;
-                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
-                if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
-            }
-            if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
-            if (ts && v == ta.sv && h == ta.sh - 1 && threadIdx.x == 0) ts[60] = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-    if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
-}
-
-int team_blocks_per_cu() {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team), 512, 0) != hipSuccess)
-        return 0;
-    return nb;
-}
-
-int launch_dec_team(const TeamArgs& a, hipStream_t s) {
-    if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
-        return set_error(LBC_E_ARG, "bad team decoder arguments");
-    hipLaunchKernelGGL(k_dec_team, dim3(a.T * a.S), dim3(512), 0, s, a);
-    return launch_status("k_dec_team");
 }
 
 __global__ void k_ctr_add(int* c, int d) { *c += d; }

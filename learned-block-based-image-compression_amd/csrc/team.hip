@@ -1,0 +1,350 @@
+// Team decoder (gfx950): lbc_decode_team's persistent raster decode of several batches in one launch.
+#include "kernels_dev.h"
+
+namespace lbic {
+
+// ----------------------------------------------------------------------------------------- team decoder
+// k_dec_team: the reference-format raster decodes of T batches in ONE persistent launch.  Team t = the S
+// workgroups with blockIdx % T == t decodes batch t (with T = 8 a team's workgroups share one XCD under the
+// observed round-robin placement: speed only, nothing depends on it).  A team runs its batch's raster steps with
+// the operations the graph decoder launches -- context net x 4, rANS, decoder x 7, recorded by the host as
+// prepared GemmArgs / RansArgs -- and a team barrier between operations instead of a kernel boundary: a raster
+// step of 12 dependent launches pays 12 barriers (one agent-scope arrival per workgroup, one polling lane) in
+// place of 12 launch boundaries, and T chains run side by side in one launch instead of one per hardware queue
+// (at most four overlap: DESIGN.md §5).
+// Hand-offs follow cdna_hip_programming.md §6 Guideline 16, R1: every value a workgroup writes for the others
+// (activations, scale indexes, y_qnt, the reconstruction and the layer-0 cache) is stored sc1 (write-through),
+// every storing wave drains (vmcnt(0)) before its workgroup's single arrival, and every load of such a value is an
+// sc1 load (buffer_load ... sc1 for the GEMM A operand, global sc1 loads for the GDN inputs and the rANS inputs);
+// weights, biases and the tables are read-only.  Every spin is bounded (TeamArgs::tmo): a workgroup that gives up
+// sets the failure word, which every other waiter reads, so the whole grid drains and the host reports an error.
+// GEMM arithmetic per output element is k_gemm_s's (KSPLIT slices, the same MFMA chains, the slice-ordered sum,
+// the shared epilogue): results are bit-identical to the graph decoder's.
+
+// A fragment of k-block kb through an sc1 (L1-bypassing) buffer load; byte offsets < 4 GB (host-checked)
+__device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
+    const int k = kb << 4;
+    gfloat_p base = rw.base[0];
+    unsigned o = rw.off[0];
+#pragma unroll
+    for (int t = 1; t < MAXSEG; ++t) {
+        const bool in = k >= rw.k0[t];
+        base = in ? rw.base[t] : base;
+        o = in ? rw.off[t] : o;
+    }
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, -1, 0x00020000);
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (o + (unsigned)(k >> 2)) << 4, 0, 16));
+}
+
+// K beyond the fast path (or more than two row tiles): each output tile (row tile mt, column tile nt) = item
+// i = nt * MT + mt, items rank, rank + S, ...; each item's slice in chunks of 8 k-blocks, no prefetch
+__device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt) {
+    constexpr int CH = 8;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
+    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
+    const BlkSrc blocks{nullptr, 1, 0, v, h};
+    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
+    int buf = 0;
+    for (int it = rank; it < items; it += S) {
+        const int mt = it % MT, nt = it / MT;
+        const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
+        const float bb = g.bias[ecol];
+        const float xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+        const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+        SRow rw;
+        small_offsets(g, bk, lane, rw);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        for (int c0 = kb0; c0 < kb1; c0 += CH) {
+            const int cn = min(CH, kb1 - c0);
+            f4 a[CH], w[CH];
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int kb = min(c0 + c, nkb - 1);
+                w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
+                a[c] = small_a_sc1(rw, kb);
+            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                f4 av = a[c];
+                if (g.square_a) av = av * av;
+                f4 t = acc;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+                acc = c < cn ? t : acc;
+            }
+        }
+        float* rb = red + buf * (KSPLIT * 256);
+        buf ^= 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x < 256) {
+            const int e = threadIdx.x;
+            float vv = rb[e];
+#pragma unroll
+            for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
+            const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
+            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx, wt);
+        }
+    }
+}
+
+// The common case: NI output tiles per workgroup (item i = nt * MT + mt; items rank, rank + S, ...; with S % MT == 0
+// every item of a workgroup has the same row tile, so its A rows are loaded once).  The NI items are unrolled
+// straight-line code (no load behind a branch: the compiler's wait after a join would count conservatively): item
+// j + 1's weight fragments are requested before item j's chain (two register buffers; one where a slice holds more
+// than 7 k-blocks, to stay within 128 VGPRs: two workgroups' worth of waves per SIMD, so the encoder's kernels fit
+// beside the persistent launch), the NI chains run back to back, and their partials meet in LDS behind ONE
+// workgroup barrier; then every thread sums and finishes its output elements.
+// ph: 0 the whole GEMM; 1 (beside the rANS decode) only the waves w < wy, whose K slices read no y_qnt, compute
+// their chains and leave the partials in LDS; 2 the remaining waves, then the reduction.
+// dts (sampled raster step, team rank 0): wave 0's s_memtime at entry, loads issued, first chain done, all chains
+// done, outputs written.
+__device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep) {
+    if (dts && threadIdx.x == 0) {
+        unsigned long long t;
+        float d;       // the v_mov reads `dep` (an MFMA result): the stamp follows its chain
+        asm volatile("v_mov_b32 %1, %2\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=v"(d) : "v"(dep) : "memory");
+        dts[p] = t;
+    }
+}
+
+template <int L, bool EXACT, int NI>
+__device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
+                                                int ph, int wy, unsigned long long* dts) {
+    constexpr int LL = EXACT ? L : L + 1;
+    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments
+    constexpr int NO = (NI * 256 + 511) / 512;   // output elements per thread
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
+    const int MT = (g.M + 15) >> 4;
+    const int mt = rank % MT;
+    const BlkSrc blocks{nullptr, 1, 0, v, h};
+    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
+    dstamp(dts, 0, 0.f);
+    float bb[NO], xx[NO];
+    if (ph != 1) {
+#pragma unroll
+        for (int q = 0; q < NO; ++q) {           // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8)
+            const int o = min((int)threadIdx.x + 512 * q, NI * 256 - 1);
+            const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
+            const int nt = (rank + j * S) / MT;
+            const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
+            bb[q] = g.bias[ecol];
+            xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+        }
+    }
+    if (act) {      // loads and chains in one branch: no join between a load and its use
+        f4 a[LL], wb[PF ? 2 : 1][LL];
+        auto issue = [&](int j, f4 (&w)[LL]) {
+            const int nt = (rank + j * S) / MT;
+#pragma unroll
+            for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
+        };
+        issue(0, wb[0]);
+        {
+            const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+            SRow rw;
+            small_offsets(g, bk, lane, rw);
+#pragma unroll
+            for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
+        }
+        dstamp(dts, 1, 0.f);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            if constexpr (PF) {
+                if (j + 1 < NI) issue(j + 1, wb[(j + 1) & 1]);
+            } else {
+                if (j > 0) issue(j, wb[0]);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
+            f4 (&w)[LL] = wb[PF ? (j & 1) : 0];
+            f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < LL; ++c) {
+                f4 av = a[c];
+                if (g.square_a) av = av * av;
+                f4 t = acc;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+                acc = c < n ? t : acc;
+            }
+            // partials -> LDS [item][slice][256]
+#pragma unroll
+            for (int i = 0; i < 4; ++i) red[(j * KSPLIT + wave) * 256 + i * 64 + lane] = acc[i];
+            if (j == 0) dstamp(dts, 2, acc[0]);
+            if (j == NI - 1) dstamp(dts, 3, acc[0]);
+        }
+    }
+    if (ph == 1) return;
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int q = 0; q < NO; ++q) {
+        const int o = threadIdx.x + 512 * q;
+        if (o >= NI * 256) break;
+        const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
+        float vv = red[j * KSPLIT * 256 + ee];
+#pragma unroll
+        for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
+        const int nt = (rank + j * S) / MT;
+        const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
+        if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb[q], xx[q], wt);
+    }
+    dstamp(dts, 4, 0.f);
+}
+
+__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
+                                              int ph = 0, int wy = 0, unsigned long long* dts = nullptr) {
+    const int nkb = g.K >> 4;
+    const int L = nkb / KSPLIT;
+    const bool exact = (nkb % KSPLIT) == 0;
+    const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
+    const int ni = rank < items ? (items - rank + S - 1) / S : 0;
+    if (ni == 0) return;
+    if (S % MT == 0 && L >= 4 && L <= 9 && ni <= (L <= 7 ? 5 : 4)) {
+        switch (L * 16 + (exact ? 8 : 0) + ni) {
+#define LBIC_N(L_, E_, N_)                                                                         \
+    case L_ * 16 + (E_ ? 8 : 0) + N_: team_gemm_items<L_, E_, N_>(g, v, h, rank, S, red, wt, ph, wy, dts); return;
+#define LBIC_E(L_, E_) LBIC_N(L_, E_, 1) LBIC_N(L_, E_, 2) LBIC_N(L_, E_, 3) LBIC_N(L_, E_, 4)
+#define LBIC_L5(L_) LBIC_E(L_, true) LBIC_E(L_, false) LBIC_N(L_, true, 5) LBIC_N(L_, false, 5)
+#define LBIC_L4(L_) LBIC_E(L_, true) LBIC_E(L_, false)
+            LBIC_L5(4) LBIC_L5(5) LBIC_L5(6) LBIC_L5(7) LBIC_L4(8) LBIC_L4(9)
+#undef LBIC_L4
+#undef LBIC_L5
+#undef LBIC_E
+#undef LBIC_N
+            default: break;
+        }
+    }
+    if (ph == 1) return;     // (the host splits a GEMM only where every workgroup takes the path above)
+    team_gemm_long(g, v, h, rank, S, red, wt);
+}
+
+// team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
+// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else)
+__device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
+                                          int* sflag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int f = 0;
+        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                f = 1;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                __hip_atomic_store((gptr<unsigned>)fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sflag = f;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
+    return *sflag == 0;
+}
+
+// ta.plain: the team's workgroups were checked (below) to share one XCD, so its L2 is the coherence point for every
+// hand-off: values are stored plain (they stay in that L2) and still loaded sc1 (past the reading CU's L1).  If
+// any team of the launch spans XCDs the launch stops before its first operation with failure word 2 and the host
+// relaunches with plain = 0 (every hand-off write-through): results never depend on placement.
+// 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch
+__global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
+    __shared__ __attribute__((aligned(16))) float red[5 * KSPLIT * 256];   // partials of up to 5 tiles
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
+    __shared__ int sflag;
+    const int T = ta.T, S = ta.S;
+    const int team = blockIdx.x % T, rank = blockIdx.x / T;
+    if (rank >= S) return;
+    unsigned* ctr = ta.sync + team * 32;
+    unsigned* fail = ta.sync + T * 32;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the recorded operations are read-only for the launch: constant address space, so their fields come in by
+    // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
+    typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
+    typedef const __attribute__((address_space(4))) RansArgs* crans_p;
+    const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
+    const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
+    unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 256 : nullptr;
+    if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
+    unsigned target = 0;
+    const bool wt = !ta.plain;
+    if (ta.plain) {
+        // placement census: every workgroup ORs its XCD into its team's word [1], then a barrier over the whole
+        // grid (counter [T * 32 + 1]); any team on more than one XCD -> every workgroup leaves
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_or((gptr<unsigned>)(ctr + 1), 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!team_sync(ta.sync + T * 32 + 1, (unsigned)(T * S), fail, ta.tmo, &sflag)) return;
+        bool local = true;
+        for (int t = 0; t < T; ++t)
+            local &= __popc(__hip_atomic_load((gptr<unsigned>)(ta.sync + t * 32 + 1), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)) == 1;
+        if (!local) {
+            if (threadIdx.x == 0) __hip_atomic_store((gptr<unsigned>)fail, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    for (int v = 0; v < ta.Hb; ++v) {
+        for (int h = 0; h < ta.Wb; ++h) {
+            const int cls = h == 0 ? 0 : h == ta.Wb - 1 ? 2 : 1;
+            const bool samp = ts && v == ta.sv && h == ta.sh;
+            for (int op = 0; op < ta.nops; ++op) {
+                const int k = ta.opk[op];
+                if (k >= 0) {
+                    team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + k), v, h, rank, S, red, wt,
+                                  op == ta.split_op ? 2 : 0, ta.split_wy, samp ? ts + 64 + op * 8 : nullptr);
+                } else {
+                    // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
+                    // the next GEMM (the decoder's first layer) that do not read y_qnt
+                    if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
+                        for (int r = rank; r < R.rows; r += S) rans_row_sparse<true>(R, lwin, r, lane, wt);
+                    } else if (ta.split_op >= 0) {
+                        team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]), v, h, rank, S, red,
+                                      wt, 1, ta.split_wy);
+                    }
+                }
+                if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
+                target += S;
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
+                if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
+            }
+            if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
+            if (ts && v == ta.sv && h == ta.sh - 1 && threadIdx.x == 0) ts[60] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
+}
+
+int team_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team), 512, 0) !=
+        hipSuccess)
+        return 0;
+    return nb;
+}
+
+int launch_dec_team(const TeamArgs& a, hipStream_t s) {
+    if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
+        return set_error(LBC_E_ARG, "bad team decoder arguments");
+    hipLaunchKernelGGL(k_dec_team, dim3(a.T * a.S), dim3(512), 0, s, a);
+    return launch_status("k_dec_team");
+}
+
+}  // namespace lbic

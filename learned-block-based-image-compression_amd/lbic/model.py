@@ -229,15 +229,24 @@ class BlockBasedImgCompLossyNetv9:
         return zhat
 
     def team_stamps(self):
-        """Raw 100 MHz stamps of the last decompress_teams launch led by this handle (LBIC_TEAM_STAMPS=1), [T, 64]
-        (lbc_team_stamps): [op] after each barrier of the sampled raster step, 60/61 the ends of the step before it
-        and of the sampled step, 62/63 launch start / end."""
+        """Raw stamps of the last decompress_teams launch led by this handle (LBIC_TEAM_STAMPS=1), [T, 256]
+        (lbc_team_stamps, 256 per team): [op] after each barrier of the sampled raster step, [32 + op] rank 0's own
+        work done, 60/61 the ends of the step before it and of the sampled step, 62/63 launch start / end (100 MHz);
+        [64 + 8 op + p] shader-clock stamps inside the operation's GEMM."""
         L = _lib.lib()
         n = ctypes.c_int(0)
         _lib.check(L.lbc_team_stamps(self._h, None, 0, ctypes.byref(n)))
         buf = (ctypes.c_ulonglong * max(n.value, 1))()
         _lib.check(L.lbc_team_stamps(self._h, buf, n.value, ctypes.byref(n)))
-        return [list(buf[i:i + 64]) for i in range(0, n.value, 64)]
+        return [list(buf[i:i + 256]) for i in range(0, n.value, 256)]
+
+    def team_stats(self):
+        """The last decompress_teams launch led by this handle (lbc_team_stats): dict(launch_ms, bytes, flops,
+        plain) -- its duration, algorithmic bytes / FLOPs, and the hand-off store mode it ran in."""
+        L = _lib.lib()
+        ms, by, fl, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _lib.check(L.lbc_team_stats(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(fl), ctypes.byref(pl)))
+        return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value)
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]

@@ -68,6 +68,17 @@ def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
         assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
 
 
+@pytest.mark.parametrize("name,T,n,shape", [("tiny_ks3311", 3, 5, (3, 4)), ("b8_lowrate_2rows", 4, 32, (2, 24))])
+def test_team_write_through_mode(name, T, n, shape, monkeypatch):
+    """LBIC_TEAM_SC1=1: every hand-off written through (k_dec_team<false>, the form that does not need a team's
+    workgroups on one XCD; the default launch reruns in it when the placement census finds a team spread out)."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_SC1", "1")
+    ref, got, _, _ = run_case(name, T, n, *shape, seed=11)
+    for t in range(T):
+        assert torch.equal(got[t], ref[t])
+
+
 @pytest.mark.parametrize("shape", [(1, 1), (1, 9), (7, 1), (3, 5), (2, 2)])
 def test_team_ragged_frames_ks3311(shape, monkeypatch):
     """One block, one row, one column, odd rectangles: the three column classes of the KS3311 step (layer-0 cache
