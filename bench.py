@@ -252,6 +252,8 @@ def main():
             v = float(t.item())
         return v
 
+    enc_acc = dict(on=False, ms=0.0, passes=0)     # HIP-event time of the encoder graphs in the timed region
+
     def compress_side(ph, xb, model=None, stream=None):
         """GPU compress on the encoder stream; symbols/indexes DMA'd into page-locked host buffers there."""
         model, stream = model or enc_model, stream or s_enc
@@ -263,8 +265,12 @@ def main():
                 h.copy_(r[k], non_blocking=True)
                 r[k] = h
             stream.synchronize()
+        e_ms = model.last_timing()[0] if enc_acc["on"] else 0.0
         with plock:
             ph["encode"] += time.perf_counter() - t0
+            if enc_acc["on"]:
+                enc_acc["ms"] += e_ms
+                enc_acc["passes"] += 1
         return r
 
     def entropy_side(r, fmt, ph, model=None):
@@ -293,7 +299,7 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, plain=[])
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[])
 
     def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
@@ -304,7 +310,11 @@ def main():
         ph = dict(encode=0.0, entropy=0.0, decode=0.0)
         if prof:
             for m_ in handles:
-                m_.profile_begin(args.sample_every)
+                m_.profile_begin(sample_every)
+            enc_acc.update(on=True, ms=0.0, passes=0)
+            # marker kernels (at::cuda spin_kernel) around the timed region: tools/kstats_summary.py restricts a
+            # rocprofv3 kernel trace of this command to the dispatches between them
+            torch.cuda._sleep(1000)
         barrier()
         t0 = time.perf_counter()
         done = dict(count=0, last=None)      # only the latest batch is kept (its pinned / device buffers)
@@ -350,6 +360,7 @@ def main():
                                 team_acc["ms"] += st_["launch_ms"]
                                 team_acc["bytes"] += st_["bytes"]
                                 team_acc["flops"] += st_["flops"]
+                                team_acc["steps"] += len(pend) * Hb * Wb
                                 team_acc["plain"].append(st_["plain"])
                             for (k_, r_, _), st_, z_ in zip(pend, sts, zs):
                                 finish(k_, r_, st_, z_)
@@ -464,6 +475,10 @@ def main():
                 th.join()
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
+        if prof:
+            enc_acc["on"] = False
+            torch.cuda._sleep(1000)
+            torch.cuda.synchronize(dev)
         ks = collect_stats() if prof else None
         if label:
             log(f"[rank {rank}] {label}: {steps} batches in {dt:.2f} s")
@@ -475,9 +490,12 @@ def main():
         return dict(value=round(world * n * H * W / (dt / k) / 1e6, 4), ms_per_step=round(dt / k * 1e3, 2),
                     steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in ph.items()}, **extra)
 
-    # sampling is part of the captured graphs: enable it before the first capture
+    # sampling is part of the captured graphs: enable it before the first capture.  The team schedule samples nothing:
+    # its decode is one persistent launch (HIP events) and the encoder graph is timed by HIP events too (in-kernel
+    # stamps on the encoder's 1,500-workgroup launches would themselves slow the sampled launches)
+    sample_every = 0 if args.team else args.sample_every
     for m_ in handles:
-        m_.profile_begin(args.sample_every)
+        m_.profile_begin(sample_every)
     if args.encode_only:      # e.g. rocprofv3 --pmc on the encoder's launch shapes
         for i in range(args.encode_only):
             compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), frames_of(i))
@@ -551,7 +569,7 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = world * n * H * W / (dt / args.steps) / 1e6
 
-    roof, kernels = roofline(kstats, dt, team_acc if args.team else None)
+    roof, kernels = roofline(kstats, dt, team_acc if args.team else None, enc_acc if args.team else None)
     mac_enc, mac_dec = arch.live_macs_per_block()
     step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
     cpu = None
@@ -619,15 +637,29 @@ def gather_records(rec, ok, dist):
     return torch.cat(allrec), bool(flag.item() == 1.0)
 
 
-def roofline(kstats, dt, team=None):
+def roofline(kstats, dt, team=None, enc=None):
     """Dominant kernel family (its time share of the timed region) against its roofline.  Graph-launched kernels:
     the in-kernel timing stamps of the sampled launches executed in the timed region (lbc_profile_*):
     `avg_launch_us` is the launch-to-launch period in the stream chain (end of the previous launch -> end of this
     one: the launch's span plus the boundary in front of it, which is what a dispatch-to-completion trace measures),
     `avg_span_us` the workgroups' own span; share = period x true launch count.  The team decoder (`team`, one
     persistent launch per group of batches): HIP events around each launch, algorithmic bytes / FLOPs per launch from
-    the library (lbc_team_stats)."""
+    the library (lbc_team_stats).  The encoder under the team schedule (`enc`, no sampling): HIP events around each
+    encoder graph divided by the graph's launches (k_gemm and its few small-M k_gemm_s ramp launches), algorithmic
+    work of all launches (lbc_kernel_stat.total_flops / total_bytes)."""
     kernels, fam = {}, {}
+    if enc is not None and kstats:
+        n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
+        if n_all and enc["ms"] > 0:
+            per = enc["ms"] / n_all
+            tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
+            tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
+            kernels["k_gemm"] = dict(launches_sampled=0, launches_total=int(n_all), avg_span_us=round(per * 1e3, 3),
+                                     avg_launch_us=round(per * 1e3, 3), est_share_of_step=round(enc["ms"] / 1e3 / dt, 4),
+                                     timing=f"HIP events around {enc['passes']} encoder graphs / their launches "
+                                            "(k_gemm + k_gemm_s ramp steps)")
+            fam["k_gemm"] = (tf / n_all, tb / n_all)
+        kstats = {}
     for name, s in (kstats or {}).items():
         span = s["total_ms"] / max(s["launches"], 1)
         per = s["total_ms_chain"] / s["launches_chain"] if s["launches_chain"] else span
@@ -645,6 +677,8 @@ def roofline(kstats, dt, team=None):
     if not kernels:
         return None, {}
     dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_total"])
+    if not fam[dom][1]:
+        return None, kernels
     per_launch_s = kernels[dom]["avg_launch_us"] * 1e-6
     fl, by = fam[dom]
     ai = fl / by if by else float("inf")
@@ -659,7 +693,9 @@ def roofline(kstats, dt, team=None):
         with open(tfile) as fh:
             pm = json.load(fh)
         f_ = re.sub(r"<.*>$", "", dom)
-        if f_ in pm and "hbm_bytes_per_dispatch" in pm[f_]:
+        if f_ == "k_dec_team" and team and "hbm_bytes_per_team_step" in pm.get(f_, {}):
+            traffic = round(pm[f_]["hbm_bytes_per_team_step"] * team["steps"] / team["launches"])
+        elif f_ in pm and "hbm_bytes_per_dispatch" in pm[f_]:
             traffic = round(pm[f_]["hbm_bytes_per_dispatch"])
     roof = dict(kernel=dom, bound=bound, achieved=round(ach, 4), peak=peak, unit=unit, frac=round(ach / peak, 5),
                 traffic=traffic, avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],

@@ -198,6 +198,9 @@ typedef struct {
     long long launches_chain; /* sampled launches whose predecessor in the stream chain was sampled too */
     double total_ms_chain;    /* summed launch-to-launch periods end(previous launch) -> end(this launch):
                                  the span plus the kernel boundary in front of it */
+    double total_flops;       /* algorithmic FLOPs / bytes of ALL launches since lbc_profile_begin (GEMM families;
+                                 sampled or not, also with sample_every = 0) */
+    double total_bytes;
 } lbc_kernel_stat;
 
 int lbc_profile_begin(lbc_model *m, int sample_every);

@@ -89,6 +89,7 @@ struct Prof {
     unsigned long long* slots = nullptr;   // device, kRanges ranges
     int range = 0, next = 0;               // slot allocation inside the range being captured
     long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
+    double work_replay[8][4][2] = {};      // their algorithmic FLOPs and bytes per replay (every launch, sampled or not)
     long long replays[8] = {};             // replays of each range's graph since lbc_profile_begin
     unsigned long long* take() {
         if (!slots || next >= kSlotsPerRange) return nullptr;
@@ -413,6 +414,7 @@ int prof_range_begin(Prof* p, int r, hipStream_t s) {
     p->range = r;
     p->next = 0;
     for (auto& c : p->per_replay[r]) c = 0;
+    for (auto& c : p->work_replay[r]) c[0] = c[1] = 0;
     if (p->sample_every && p->slots)
         return launch_zero_u64(p->slots + kSlotU64 * (size_t)r * kSlotsPerRange, kSlotU64 * kSlotsPerRange, s);
     return LBC_OK;
@@ -427,6 +429,12 @@ struct Recorder {
 static thread_local Recorder* g_rec = nullptr;
 
 // launch a GEMM; in a sampled step give it a timing slot and record its algorithmic work
+static void gemm_work(const GemmArgs& g, int k_live, double& flops, double& bytes) {
+    const double K = k_live > 0 ? k_live : g.K;
+    flops = 2.0 * g.M * K * g.N;
+    bytes = 4.0 * (K * g.N + (double)g.M * K + (double)g.M * g.N * (g.square_a ? 2 : 1));
+}
+
 int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     if (g_rec) {
         GemmArgs g = g0;
@@ -438,7 +446,14 @@ int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
         return LBC_OK;
     }
     Prof* p = g_prof;
-    if (p) p->per_replay[p->range][gemm_class(g0)] += 1;   // the class launch_gemm will pick
+    if (p) {
+        const int c = gemm_class(g0);       // the class launch_gemm will pick
+        double f, b;
+        gemm_work(g0, k_live, f, b);
+        p->per_replay[p->range][c] += 1;
+        p->work_replay[p->range][c][0] += f;
+        p->work_replay[p->range][c][1] += b;
+    }
     if (!p || !p->active) return launch_gemm(g0, s);
     GemmArgs g = g0;
     g.ts = p->take();
@@ -446,9 +461,8 @@ int gemm(const GemmArgs& g0, hipStream_t s, int k_live = -1) {
     int cls = 0;
     int rc = launch_gemm(g, s, &cls);
     if (rc) return rc;
-    const double K = k_live > 0 ? k_live : g.K;
-    const double flops = 2.0 * g.M * K * g.N;
-    const double bytes = 4.0 * (K * g.N + (double)g.M * K + (double)g.M * g.N * (g.square_a ? 2 : 1));
+    double flops, bytes;
+    gemm_work(g, k_live, flops, bytes);
     p->add(cls, g.ts, flops, bytes);
     return LBC_OK;
 }
@@ -1318,7 +1332,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     HIPCHK(hipSetDevice(dev));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_cu = team_blocks_per_cu();
-    int S = std::min(32, cus / T);
+    int S = std::min(32, cus / TEAM_MAX);     // grid 8 x S: one XCD slot per team (k_dec_team)
     if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
     if (S < 1 || per_cu < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     for (int t = 0; t < T; ++t) {
@@ -1706,12 +1720,16 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
     // true launch counts since lbc_profile_begin (the stamps are a sample of them)
     for (int c = 0; c < 4; ++c) {
         long long tot = 0;
-        for (int r = 0; r < 8; ++r) tot += p.per_replay[r][c] * p.replays[r];
+        for (int r = 0; r < 8; ++r) {
+            tot += p.per_replay[r][c] * p.replays[r];
+            acc[c].total_flops += p.work_replay[r][c][0] * p.replays[r];
+            acc[c].total_bytes += p.work_replay[r][c][1] * p.replays[r];
+        }
         acc[c].total_launches = tot;
     }
     int n = 0;
     for (int c = 0; c < 4 && n < max_out; ++c)
-        if (acc[c].launches) out[n++] = acc[c];
+        if (acc[c].launches || acc[c].total_launches) out[n++] = acc[c];
     *n_out = n;
     return LBC_OK;
 }

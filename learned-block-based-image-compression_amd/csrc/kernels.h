@@ -103,8 +103,8 @@ struct RansArgs {
     int sparse;              // 1: k_rans_decode_sparse (centre-interval fast path, tables read from global memory)
 };
 
-// Team decoder (k_dec_team, kernels.hip): the raster decodes of T batches in ONE persistent launch, S workgroups
-// per batch ("team"), team barriers between the recorded operations of a raster step instead of kernel boundaries
+// Team decoder (k_dec_team, team.hip): the raster decodes of T <= 8 batches in ONE persistent launch, S workgroups
+// per batch ("team", the workgroups of one blockIdx % 8 slot), team barriers between the recorded operations of a raster step instead of kernel boundaries
 constexpr int TEAM_MAX = 8;        // teams per launch
 constexpr int TEAM_MAXOPS = 24;    // operations per raster step
 struct TeamArgs {

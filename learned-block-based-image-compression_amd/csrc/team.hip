@@ -4,9 +4,9 @@
 namespace lbic {
 
 // ----------------------------------------------------------------------------------------- team decoder
-// k_dec_team: the reference-format raster decodes of T batches in ONE persistent launch.  Team t = the S
-// workgroups with blockIdx % T == t decodes batch t (with T = 8 a team's workgroups share one XCD under the
-// observed round-robin placement: speed only, nothing depends on it).  A team runs its batch's raster steps with
+// k_dec_team: the reference-format raster decodes of T <= 8 batches in ONE persistent launch.  Team t = the S
+// workgroups with blockIdx % 8 == t decodes batch t (a team's workgroups share one XCD under the observed round-robin
+// placement: speed, and plain hand-off stores once the census below has confirmed it; nothing else depends on it).  A team runs its batch's raster steps with
 // the operations the graph decoder launches -- context net x 4, rANS, decoder x 7, recorded by the host as
 // prepared GemmArgs / RansArgs -- and a team barrier between operations instead of a kernel boundary: a raster
 // step of 12 dependent launches pays 12 barriers (one agent-scope arrival per workgroup, one polling lane) in
@@ -270,8 +270,10 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
     __shared__ int sflag;
     const int T = ta.T, S = ta.S;
-    const int team = blockIdx.x % T, rank = blockIdx.x / T;
-    if (rank >= S) return;
+    // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
+    // whatever T is); the others leave at once
+    const int team = blockIdx.x & 7, rank = blockIdx.x >> 3;
+    if (team >= T || rank >= S) return;
     unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
@@ -343,7 +345,7 @@ int team_blocks_per_cu() {
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
         return set_error(LBC_E_ARG, "bad team decoder arguments");
-    hipLaunchKernelGGL(k_dec_team, dim3(a.T * a.S), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(k_dec_team, dim3(8 * a.S), dim3(512), 0, s, a);
     return launch_status("k_dec_team");
 }
 

@@ -20,7 +20,8 @@ class LbcKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_longlong), ("total_launches", ctypes.c_longlong),
                 ("total_ms", ctypes.c_double),
                 ("flops", ctypes.c_double), ("bytes", ctypes.c_double),
-                ("launches_chain", ctypes.c_longlong), ("total_ms_chain", ctypes.c_double)]
+                ("launches_chain", ctypes.c_longlong), ("total_ms_chain", ctypes.c_double),
+                ("total_flops", ctypes.c_double), ("total_bytes", ctypes.c_double)]
 
 
 class LbcConfig(ctypes.Structure):

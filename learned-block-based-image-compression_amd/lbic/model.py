@@ -317,7 +317,8 @@ class BlockBasedImgCompLossyNetv9:
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_launches=arr[i].total_launches,
                                            total_ms=arr[i].total_ms, flops=arr[i].flops, bytes=arr[i].bytes,
                                            launches_chain=arr[i].launches_chain,
-                                           total_ms_chain=arr[i].total_ms_chain)
+                                           total_ms_chain=arr[i].total_ms_chain, total_flops=arr[i].total_flops,
+                                           total_bytes=arr[i].total_bytes)
                 for i in range(n.value)}
 
     def last_timing(self):

@@ -21,6 +21,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p
     python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 "$@" > $O/bench_rocprof_$TAG.log 2>&1 || rc=$?
 # (no further GPU step after a failure; the summaries are copied either way)
 cp $(find /tmp/pk_$TAG -name "*kernel_stats.csv") $O/kernel_stats_$TAG.csv || true
-python3 $R/tools/kstats_summary.py $O/kernel_stats_$TAG.csv > $O/kernel_stats_$TAG.txt || true
+python3 $R/tools/kstats_summary.py $O/kernel_stats_$TAG.csv $(find /tmp/pk_$TAG -name "*kernel_trace.csv" | head -1) \
+    > $O/kernel_stats_$TAG.txt || true
 echo "done rc=$rc"
 exit $rc

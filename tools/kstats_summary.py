@@ -1,9 +1,10 @@
 """Summarise a rocprofv3 --kernel-trace --stats CSV (run_kernel_stats.csv) per kernel family.
 
-usage: python tools/kstats_summary.py kernel_stats.csv
+usage: python tools/kstats_summary.py kernel_stats.csv [kernel_trace.csv]
 Prints, per family (template arguments dropped: k_gemm_s, k_gemm, k_rans_decode, ...), the call count, the
-total and the average dispatch-to-completion duration in microseconds -- the figures bench.py's roofline
-(avg_launch_us of the dominant family) must agree with.
+total and the average dispatch-to-completion duration in microseconds over the whole command; with the
+kernel trace also the same table for the dispatches inside bench.py's timed region (between its two
+spin_kernel markers) -- the figures bench.py's roofline (avg_launch_us of the dominant family) must agree with.
 """
 import csv
 import re
@@ -29,5 +30,32 @@ def main(path):
         print(f"{f:32s} {c:10d} {t / 1e6:10.2f} {t / c / 1e3:8.3f}")
 
 
+def region(path):
+    rows = list(csv.DictReader(open(path)))
+    if not rows:
+        return
+    kn = next(k for k in rows[0] if "Name" in k and "Kernel" in k)
+    ks = next(k for k in rows[0] if "Start" in k)
+    ke = next(k for k in rows[0] if "End" in k)
+    spins = sorted((int(r[ks]), int(r[ke])) for r in rows if "spin_kernel" in r[kn])
+    if len(spins) < 2:
+        print("(no timed-region markers in the trace)")
+        return
+    t0, t1 = spins[0][1], spins[-1][0]
+    fam = defaultdict(lambda: [0, 0.0])
+    for r in rows:
+        s_, e_ = int(r[ks]), int(r[ke])
+        if t0 <= s_ and e_ <= t1 and "spin_kernel" not in r[kn]:
+            f = family(r[kn])
+            fam[f][0] += 1
+            fam[f][1] += e_ - s_
+    print(f"\ntimed region only ({(t1 - t0) / 1e9:.3f} s between the markers)")
+    print(f"{'family':32s} {'calls':>10s} {'total_ms':>10s} {'avg_us':>8s}")
+    for f, (c, t) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        print(f"{f:32s} {c:10d} {t / 1e6:10.2f} {t / c / 1e3:8.3f}")
+
+
 if __name__ == "__main__":
     main(sys.argv[1])
+    if len(sys.argv) > 2:
+        region(sys.argv[2])
