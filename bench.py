@@ -69,8 +69,10 @@ def log(*a):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed batches (each encoded and decoded in the region)")
-    ap.add_argument("--warmup", type=int, default=5, help="untimed pipeline batches before the timed region")
+    ap.add_argument("--steps", type=int, default=32,
+                    help="timed batches (each encoded and decoded in the region; the pipeline's fill and drain -- the "
+                         "first group's encodes and the last group's decode launch -- are inside it)")
+    ap.add_argument("--warmup", type=int, default=8, help="untimed pipeline batches before the timed region")
     ap.add_argument("--batch", type=int, default=32, help="frames per batch (per GPU)")
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
     ap.add_argument("--height", type=int, default=0, help="frame height (default: --size)")

@@ -1411,6 +1411,12 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.Hb = Hb;
         a.Wb = Wb;
         a.sync = m0->team_sync.as<unsigned>();
+        // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
+        a.ni_max = 2;
+        for (const GemmArgs& d : gem) {
+            const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
+            if (team_fast_path(d, S)) a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
+        }
         // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices
         // that end before it run beside the rANS decode when every workgroup takes the fast path for it
         a.split_op = -1;

@@ -107,6 +107,7 @@ struct RansArgs {
 // per batch ("team", the workgroups of one blockIdx % 8 slot), team barriers between the recorded operations of a raster step instead of kernel boundaries
 constexpr int TEAM_MAX = 8;        // teams per launch
 constexpr int TEAM_MAXOPS = 24;    // operations per raster step
+constexpr int TEAM_NI_MAX = 6;     // output tiles per workgroup and GEMM on the team kernel's fast path
 struct TeamArgs {
     const GemmArgs* gemm;    // [T][3][NG] prepared GEMMs of one raster step, per team and column class
                              // (0: h = 0, 1: 0 < h < Wb - 1, 2: h = Wb - 1); block rows / columns set in-kernel
@@ -117,6 +118,7 @@ struct TeamArgs {
                              // [T * 32] the failure word (1 timeout, 2 a team spans XCDs) and [T * 32 + 1] the
                              // census barrier; zeroed before every launch
     int plain;               // 1: plain hand-off stores (needs every team on one XCD: checked in-kernel)
+    int ni_max;              // most output tiles one workgroup computes in one GEMM of the step (LDS for partials)
     int split_op, split_wy;  // split_op >= 0: the GEMM after the rANS decode; its K slices w < split_wy (no y_qnt)
                              // run beside the rANS decode, the rest after it
     unsigned long long tmo;  // s_memrealtime ticks (100 MHz) one barrier waits before the launch gives up
@@ -125,10 +127,10 @@ struct TeamArgs {
     int sv, sh;
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
-inline bool team_fast_path(const GemmArgs& g, int S) {
+__host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
     const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
     const int ni = (items + S - 1) / S;
-    return S % MT == 0 && L >= 4 && L <= 9 && ni <= (L <= 7 ? 5 : 4);
+    return S % MT == 0 && L >= 4 && L <= 9 && ni <= TEAM_NI_MAX;
 }
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch

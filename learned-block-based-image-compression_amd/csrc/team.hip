@@ -95,32 +95,36 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
     }
 }
 
-// The common case: NI output tiles per workgroup (item i = nt * MT + mt; items rank, rank + S, ...; with S % MT == 0
-// every item of a workgroup has the same row tile, so its A rows are loaded once).  The NI items are unrolled
-// straight-line code (no load behind a branch: the compiler's wait after a join would count conservatively): item
-// j + 1's weight fragments are requested before item j's chain (two register buffers; one where a slice holds more
-// than 7 k-blocks, to stay within 128 VGPRs: two workgroups' worth of waves per SIMD, so the encoder's kernels fit
-// beside the persistent launch), the NI chains run back to back, and their partials meet in LDS behind ONE
-// workgroup barrier; then every thread sums and finishes its output elements.
+// The common case: ni <= TEAM_NI_MAX output tiles per workgroup (item i = nt * MT + mt; items rank, rank + S, ...;
+// with S % MT == 0 every item of a workgroup has the same row tile, so its A rows are loaded once).  Item j + 1's
+// weight fragments are requested before item j's chain (two register buffers; one where a slice holds more than 7
+// k-blocks, to stay within 128 VGPRs), unconditionally (the last request repeats the last item) so that no load sits
+// behind a branch (the compiler's wait after such a join counts conservatively and serialises the prefetch); the
+// chains run back to back, and their partials meet in LDS behind ONE workgroup barrier; then every thread sums and
+// finishes its output elements.
 // ph: 0 the whole GEMM; 1 (beside the rANS decode) only the waves w < wy, whose K slices read no y_qnt, compute
 // their chains and leave the partials in LDS; 2 the remaining waves, then the reduction.
-// dts (sampled raster step, team rank 0): wave 0's s_memtime at entry, loads issued, first chain done, all chains
-// done, outputs written.
+// dts (sampled raster step, team rank 0; LBIC_TEAM_DIAG builds): wave 0's s_memtime at entry, loads issued, first
+// chain done, all chains done, outputs written.
 __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep) {
+#ifndef LBIC_TEAM_DIAG
+    (void)dts; (void)p; (void)dep;      // diagnostic build only (make team_diag): keeps the item loop's registers free
+#else
     if (dts && threadIdx.x == 0) {
         unsigned long long t;
         float d;       // the v_mov reads `dep` (an MFMA result): the stamp follows its chain
         asm volatile("v_mov_b32 %1, %2\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=v"(d) : "v"(dep) : "memory");
         dts[p] = t;
     }
+#endif
 }
 
-template <int L, bool EXACT, int NI>
-__device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
-                                                int ph, int wy, unsigned long long* dts) {
+template <int L, bool EXACT>
+__device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int ni, float* red,
+                                                bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
     constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments
-    constexpr int NO = (NI * 256 + 511) / 512;   // output elements per thread
+    constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = g.K >> 4;
@@ -131,12 +135,13 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
+    const int nout = ni * 256;
     dstamp(dts, 0, 0.f);
-    float bb[NO], xx[NO];
+    float bb[NOMAX], xx[NOMAX];
     if (ph != 1) {
 #pragma unroll
-        for (int q = 0; q < NO; ++q) {           // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8)
-            const int o = min((int)threadIdx.x + 512 * q, NI * 256 - 1);
+        for (int q = 0; q < NOMAX; ++q) {        // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
+            const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NOMAX
             const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
             const int nt = (rank + j * S) / MT;
             const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
@@ -145,30 +150,14 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         }
     }
     if (act) {      // loads and chains in one branch: no join between a load and its use
-        f4 a[LL], wb[PF ? 2 : 1][LL];
+        f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
             const int nt = (rank + j * S) / MT;
 #pragma unroll
             for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
         };
-        issue(0, wb[0]);
-        {
-            const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
-            SRow rw;
-            small_offsets(g, bk, lane, rw);
-#pragma unroll
-            for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
-        }
-        dstamp(dts, 1, 0.f);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-            if constexpr (PF) {
-                if (j + 1 < NI) issue(j + 1, wb[(j + 1) & 1]);
-            } else {
-                if (j > 0) issue(j, wb[0]);
-            }
+        auto chain = [&](int j, f4 (&w)[LL]) {
             __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
-            f4 (&w)[LL] = wb[PF ? (j & 1) : 0];
             f4 acc = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < LL; ++c) {
@@ -183,16 +172,43 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 #pragma unroll
             for (int i = 0; i < 4; ++i) red[(j * KSPLIT + wave) * 256 + i * 64 + lane] = acc[i];
             if (j == 0) dstamp(dts, 2, acc[0]);
-            if (j == NI - 1) dstamp(dts, 3, acc[0]);
+            if (j == ni - 1) dstamp(dts, 3, acc[0]);
+        };
+        issue(0, w0);
+        {
+            const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+            SRow rw;
+            small_offsets(g, bk, lane, rw);
+#pragma unroll
+            for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
+        }
+        dstamp(dts, 1, 0.f);
+        // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
+        // hit) so that no load sits behind a branch
+        if constexpr (PF) {
+            for (int j = 0;;) {
+                issue(min(j + 1, ni - 1), w1);
+                chain(j, w0);
+                if (++j >= ni) break;
+                issue(min(j + 1, ni - 1), w0);
+                chain(j, w1);
+                if (++j >= ni) break;
+            }
+        } else {
+            for (int j = 0;;) {
+                chain(j, w0);
+                if (++j >= ni) break;
+                issue(j, w0);
+            }
         }
     }
     if (ph == 1) return;
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int q = 0; q < NO; ++q) {
+    for (int q = 0; q < NOMAX; ++q) {
         const int o = threadIdx.x + 512 * q;
-        if (o >= NI * 256) break;
+        if (o >= nout) break;
         const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
         float vv = red[j * KSPLIT * 256 + ee];
 #pragma unroll
@@ -212,17 +228,12 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
     const int ni = rank < items ? (items - rank + S - 1) / S : 0;
     if (ni == 0) return;
-    if (S % MT == 0 && L >= 4 && L <= 9 && ni <= (L <= 7 ? 5 : 4)) {
-        switch (L * 16 + (exact ? 8 : 0) + ni) {
-#define LBIC_N(L_, E_, N_)                                                                         \
-    case L_ * 16 + (E_ ? 8 : 0) + N_: team_gemm_items<L_, E_, N_>(g, v, h, rank, S, red, wt, ph, wy, dts); return;
-#define LBIC_E(L_, E_) LBIC_N(L_, E_, 1) LBIC_N(L_, E_, 2) LBIC_N(L_, E_, 3) LBIC_N(L_, E_, 4)
-#define LBIC_L5(L_) LBIC_E(L_, true) LBIC_E(L_, false) LBIC_N(L_, true, 5) LBIC_N(L_, false, 5)
-#define LBIC_L4(L_) LBIC_E(L_, true) LBIC_E(L_, false)
-            LBIC_L5(4) LBIC_L5(5) LBIC_L5(6) LBIC_L5(7) LBIC_L4(8) LBIC_L4(9)
-#undef LBIC_L4
-#undef LBIC_L5
-#undef LBIC_E
+    if (team_fast_path(g, S)) {
+        switch (L * 2 + (exact ? 1 : 0)) {
+#define LBIC_N(L_)                                                                                     \
+    case L_ * 2 + 1: team_gemm_items<L_, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts); return;      \
+    case L_ * 2: team_gemm_items<L_, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts); return;
+            LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
             default: break;
         }
@@ -266,9 +277,12 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // relaunches with plain = 0 (every hand-off write-through): results never depend on placement.
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch
 __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
-    __shared__ __attribute__((aligned(16))) float red[5 * KSPLIT * 256];   // partials of up to 5 tiles
-    __shared__ __attribute__((aligned(16))) uint32_t lwin[RANS_WIN];
-    __shared__ int sflag;
+    // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
+    // [rANS window RANS_WIN words][barrier flag, padded to 16 B][GEMM partials ni_max x KSPLIT x 256 floats]
+    extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
+    uint32_t* lwin = team_lds;
+    int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN);
+    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + 4);
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
@@ -345,7 +359,15 @@ int team_blocks_per_cu() {
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
         return set_error(LBC_E_ARG, "bad team decoder arguments");
-    hipLaunchKernelGGL(k_dec_team, dim3(8 * a.S), dim3(512), 0, s, a);
+    if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_team), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        return true;
+    }();
+    (void)attr;
+    const size_t lds = (size_t)(RANS_WIN + 4) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4;
+    hipLaunchKernelGGL(k_dec_team, dim3(8 * a.S), dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 
