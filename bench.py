@@ -85,6 +85,9 @@ def parse_args(argv=None):
                     help="headline schedule: one encoder handle compresses the batches while groups of TEAM encoded "
                          "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
                          "workgroups per 32-frame batch); 0 = the --workers / --depth schedules")
+    ap.add_argument("--team-groups", default="last-full", choices=("last-full", "first-full"),
+                    help="when --steps is not a multiple of --team: the partial group is the first launch (last-full) "
+                         "or the last one (first-full)")
     ap.add_argument("--workers", type=int, default=4,
                     help="headline schedule: W workers, each (own handle + stream + thread) compressing, entropy coding "
                          "and decoding whole batches (0 = the encoder + --depth decoders pipeline)")
@@ -341,14 +344,23 @@ def main():
                     team_acc[kk] = [] if kk == "plain" else 0
             errs = []
 
+            # group sizes: with --team-groups last-full (default) a partial group comes FIRST, so the launch that
+            # runs alone after the last encode (the drain) is a full one and the first launch starts earlier
+            nfull, rem = divmod(steps, team)
+            sizes = ([rem] if rem else []) + [team] * nfull
+            if args.team_groups == "first-full":
+                sizes = sizes[::-1]
+
             def team_decoder():
                 pend = []
+                gi = 0
                 try:
                     while True:
                         it = dq.get()
                         if it is not None:
                             pend.append(it)
-                        if pend and (it is None or len(pend) == team):
+                        if pend and (it is None or len(pend) == sizes[min(gi, len(sizes) - 1)]):
+                            gi += 1
                             t0_ = time.perf_counter()
                             sts = [f_.result() for (_, _, f_) in pend]
                             with torch.cuda.stream(s_decs[0]):

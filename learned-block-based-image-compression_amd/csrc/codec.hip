@@ -1451,6 +1451,8 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     a.tmo = 100000000ull;                    // 1 s at one barrier: far above any operation's time
     const char* st = getenv("LBIC_TEAM_STAMPS");
     a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
+    const char* pfe = getenv("LBIC_TEAM_PF");   // weight tiles of the next GEMM requested at each barrier (0..2)
+    a.pf = pfe ? std::max(0, std::min(2, atoi(pfe))) : 0;
     a.sv = Hb / 2;
     a.sh = Wb / 2;
     for (int t = 0; t < T; ++t) {

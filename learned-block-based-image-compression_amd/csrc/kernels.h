@@ -125,6 +125,8 @@ struct TeamArgs {
     unsigned long long* ts;  // optional [T][256]: s_memrealtime after every barrier of raster step (sv, sh), then
                              // [64 + 8 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
     int sv, sh;
+    int pf;                  // weight tiles of the NEXT operation each workgroup requests while it waits at a team
+                             // barrier (0 = none): they arrive in the team's L2 before the operation starts
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {

@@ -21,8 +21,10 @@ namespace lbic {
 
 // CH k-blocks per chunk: all their loads are issued together, and chunk c+1 is in flight while chunk c
 // is multiplied, so a slice of K costs about one memory round trip instead of one per k-block.
-template <int BM, int BN, int NW, int CH>
-__global__ __launch_bounds__(NW * 64) void k_gemm(const GemmArgs g) {
+// OCC: minimum waves per SIMD the register allocation must allow (1 = no constraint).  The team decoder keeps
+// 256 of each SIMD's 512 VGPRs while it runs, so the encoder's residency beside it is (512 - 256) / its VGPRs.
+template <int BM, int BN, int NW, int CH, int OCC = 1>
+__global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     constexpr int MS = BM / 16, NS = BN / 16, SPW = KSPLIT / NW;
     extern __shared__ __attribute__((aligned(16))) float red[];
     warm_kernargs<10>();
@@ -269,12 +271,12 @@ static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B 
 }
 static const int g_exact = exact_on();
 
-template <int BM, int BN, int NW, int CH>
+template <int BM, int BN, int NW, int CH, int OCC = 1>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "LDS request above 160 KB");
     static const bool attr = [] {     // once per instantiation (thread-safe static initialisation)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH, OCC>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -282,7 +284,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     GemmArgs gs = g;
     gs.swz = g_enc_swz;
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH>), grid, dim3(NW * 64), lds, s, gs);
+    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, gs);
     return launch_status("k_gemm");
 }
 
@@ -355,17 +357,29 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         return launch_status("k_gemm_s");
     }
     if (cfg_id) *cfg_id = 1;
-    // Encoder wavefront steps (n_img images x up to 48 blocks): many small tiles beat few large ones
-    // (measured encode time per 32-frame batch, encoder alone: 64x32 / 4 waves 149 ms, 32x32 121, 16x32 / 4
-    // waves 114, 16x32 / 8 waves 112): the per-tile K loop is latency-bound, so the step wants more
-    // workgroups.  Beside the two ganged decode passes (4 batches per encoder pass) 16x32 / 4 waves (each wave
-    // two K slices) takes 77 us per launch against 122 us for 8 waves: encode phase 100 vs 150 ms per batch.
-    // LBIC_ENC_CFG selects the other shapes for A/B runs (results are identical for every shape).
+    // Encoder wavefront steps (n_img images x up to 48 blocks): many small tiles beat few large ones; the per-tile K
+    // loop is latency-bound, so the step wants workgroups and waves.  Measured encode time per 32-frame 768x768
+    // batch, encoder alone (tools/enc_exp.py, profiles/r02_exp/encoder_occupancy.txt), every shape bit-identical:
+    // 16x32 / 8 waves / one k-block per chunk (56 VGPRs: 8 waves per SIMD) 98.7 ms; 16x32 / 4 waves / 2-block
+    // chunks 108.2 (round 2's earlier default, 86 VGPRs: 5 waves per SIMD, 2 beside the team decoder's 256 VGPRs);
+    // 16x32 / 4 / 1 capped at 70 VGPRs 105.7; 32x32 / 8 / 1 107.5; 16x64 / 8 / 1 112.0; 16x16 / 4 / 1 122.3;
+    // register caps that spill (64 / 80 VGPRs) 116.7 / 115.8.  Beside the team decoder (bench.py --steps 20):
+    // 84.9 Mpix/s against 79.7 for the earlier default.  LBIC_ENC_CFG selects the others for A/B runs.
     switch (g_enc_cfg) {
         case 1: return launch_cfg<64, 32, 4, 2>(g, s);
         case 2: return launch_cfg<16, 32, 8, 2>(g, s);
         case 3: return launch_cfg<32, 32, 8, 2>(g, s);
-        default: return launch_cfg<16, 32, 4, 2>(g, s);
+        case 4: return launch_cfg<16, 32, 4, 1, 8>(g, s);     // <= 64 VGPRs (spills)
+        case 5: return launch_cfg<16, 32, 4, 2, 6>(g, s);     // <= 80 VGPRs (spills)
+        case 6: return launch_cfg<16, 32, 4, 1, 6>(g, s);
+        case 8: return launch_cfg<16, 32, 4, 1, 1>(g, s);
+        case 9: return launch_cfg<32, 32, 4, 1, 1>(g, s);
+        case 10: return launch_cfg<16, 64, 4, 1, 1>(g, s);
+        case 11: return launch_cfg<16, 16, 4, 1, 1>(g, s);
+        case 12: return launch_cfg<16, 64, 8, 1, 1>(g, s);
+        case 13: return launch_cfg<32, 32, 8, 1, 1>(g, s);
+        case 15: return launch_cfg<16, 32, 4, 2>(g, s);
+        default: return launch_cfg<16, 32, 8, 1>(g, s);    // 0 and 7
     }
 }
 

@@ -119,7 +119,7 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 #endif
 }
 
-template <int L, bool EXACT>
+template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int ni, float* red,
                                                 bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
@@ -162,7 +162,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 #pragma unroll
             for (int c = 0; c < LL; ++c) {
                 f4 av = a[c];
-                if (g.square_a) av = av * av;
+                if constexpr (SQ) av = av * av;     // GDN: squared A (a compile-time choice: no select, no temporaries)
                 f4 t = acc;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
@@ -231,8 +231,14 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     if (team_fast_path(g, S)) {
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                     \
-    case L_ * 2 + 1: team_gemm_items<L_, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts); return;      \
-    case L_ * 2: team_gemm_items<L_, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts); return;
+    case L_ * 2 + 1:                                                                                   \
+        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);     \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);              \
+        return;                                                                                        \
+    case L_ * 2:                                                                                       \
+        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);    \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);             \
+        return;
             LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
             default: break;
@@ -242,15 +248,52 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     team_gemm_long(g, v, h, rank, S, red, wt);
 }
 
+// The weight fragments of the first NIT items this workgroup computes in GEMM g (each wave: its K slice), requested
+// while the workgroup waits at the team barrier in front of g (weights are read-only: no ordering against the
+// barrier is needed).  The values are folded into one LDS word nobody reads, so the loads are kept; the wave waits
+// for them at the barrier's closing __syncthreads, i.e. crossing the barrier costs max(barrier, fetch).
+template <int NIT>
+__device__ __forceinline__ void team_prefetch(const GemmArgs& g, int rank, int S, float* sink) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = g.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
+    const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
+    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
+    f4 w[NIT][10];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+        const int nt = min(rank + j * S, items - 1) / MT;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) w[j][c] = Wt[((long)min(kb0 + c, kb1 - 1) * g.NB16 + nt) * 64];
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NIT; ++j)
+#pragma unroll
+        for (int c = 0; c < 10; ++c) s += w[j][c][0];
+    if (lane == 0) sink[wave] = s;
+}
+
+__device__ __forceinline__ void team_prefetch_any(const GemmArgs* g, int rank, int S, int nit, float* sink) {
+    if (!g || rank >= (((g->M + 15) >> 4) * ((g->N + 15) >> 4))) return;
+    if (nit >= 2) team_prefetch<2>(*g, rank, S, sink);
+    else team_prefetch<1>(*g, rank, S, sink);
+}
+
 // team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
-// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else)
+// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else).  pf: the next
+// GEMM, whose first weight tiles are requested after the arrival (team_prefetch)
 __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
-                                          int* sflag) {
+                                          int* sflag, const GemmArgs* pf = nullptr, int rank = 0, int S = 1,
+                                          int npf = 0, float* sink = nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
     __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (npf) team_prefetch_any(pf, rank, S, npf, sink);
     if (threadIdx.x == 0) {
         int f = 0;
-        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -278,11 +321,12 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch
 __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
-    // [rANS window RANS_WIN words][barrier flag, padded to 16 B][GEMM partials ni_max x KSPLIT x 256 floats]
+    // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
     uint32_t* lwin = team_lds;
     int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN);
-    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + 4);
+    float* sink = reinterpret_cast<float*>(team_lds + RANS_WIN + 4);     // team_prefetch's unread word per wave
+    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + 12);
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
@@ -338,7 +382,17 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
                 target += S;
-                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
+                const GemmArgs* nx = nullptr;
+                if (ta.pf) {     // the GEMM after this barrier (the next step's first at the step's end)
+                    int nop = op + 1, ncls = cls;
+                    if (nop == ta.nops) {
+                        nop = 0;
+                        const int hn = h + 1 == ta.Wb ? 0 : h + 1;
+                        ncls = hn == 0 ? 0 : hn == ta.Wb - 1 ? 2 : 1;
+                    }
+                    if (ta.opk[nop] >= 0) nx = (const GemmArgs*)(G + ncls * ta.NG + ta.opk[nop]);
+                }
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag, nx, rank, S, ta.pf, sink)) return;
                 if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
             }
             if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
@@ -366,7 +420,7 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
         return true;
     }();
     (void)attr;
-    const size_t lds = (size_t)(RANS_WIN + 4) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4;
+    const size_t lds = (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4;
     hipLaunchKernelGGL(k_dec_team, dim3(8 * a.S), dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }

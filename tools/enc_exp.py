@@ -40,7 +40,7 @@ def main():
     h = hashlib.sha256()
     for k in ("symbols", "indexes", "zhat"):
         h.update(r[k].cpu().numpy().tobytes())
-    print(json.dumps(dict(tiled=os.environ.get("LBIC_ENC_TILED", "default"), encode_ms=[round(t, 2) for t in ts],
+    print(json.dumps(dict(tiled=os.environ.get("LBIC_ENC_TILED", "default"), cfg=os.environ.get("LBIC_ENC_CFG", "0"), encode_ms=[round(t, 2) for t in ts],
                           digest=h.hexdigest()[:16])), flush=True)
 
 
