@@ -41,6 +41,20 @@ int set_error(int code, const std::string& msg) {
         if (e_ != hipSuccess) return set_error(LBC_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+static int hip_rc(hipError_t e) {   // for code that must not return early (inside a stream capture)
+    return e == hipSuccess ? LBC_OK : set_error(LBC_E_HIP, hipGetErrorString(e));
+}
+
+// Encoder graph fork: each wavefront step's context net (4 GEMMs) and the transform's first six GEMMs are independent
+// (only the quantising GEMM reads the means / scales), so they are captured as two branches joined before it.
+// Encoder alone 98.7 -> 95.0 ms per 32-frame batch, bit-identical; beside the team decoder within noise (+0.3..0.9 %;
+// profiles/r02_exp/encoder_fork_team.txt).  LBIC_ENC_FORK=0: one chain (with four busy streams, the workers schedule,
+// the branch's extra hardware queue cost 5 %: profiles/r02_exp/encoder_fork.txt).
+static bool enc_fork_on() {
+    const char* e = getenv("LBIC_ENC_FORK");
+    return !e || atoi(e) != 0;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -174,6 +188,10 @@ struct lbc_model {
     std::vector<long long> enc_key, dec_key, wf_key;
     DevBuf x_in, sym_buf, idx_buf, bits_buf, ctr;
     hipStream_t cap = nullptr;
+    // encoder graph fork (LBIC_ENC_FORK=1): each wavefront step's context net is captured on cap2, beside the
+    // encoder transform's first six GEMMs on cap; the quantising GEMM joins both
+    hipStream_t cap2 = nullptr;
+    hipEvent_t fev[2] = {nullptr, nullptr};
     // band pipeline (lbc_band_*): this handle codes block rows [band_v0, band_v0 + ws_Hb) of taller frames;
     // one captured graph per range of global wavefront steps
     int band_v0 = -1;
@@ -391,6 +409,8 @@ int prepare_device(lbc_model* m) {
         // (lane streams are created only when a decode uses several lanes: every stream a process creates
         // takes a turn on its few hardware queues, and two busy streams on one queue serialise)
         HIPCHK(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&m->cap2, hipStreamNonBlocking));
+        for (auto& e : m->fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     if (m->tabs_dirty) {
         int rc;
@@ -706,10 +726,13 @@ int run_dec(lbc_model* m, Work& w, GemmArgs g, hipStream_t s, float* xhat = null
     return run_dense(g, m->net->d3, d1, W, EPI_CLAMPZ, nullptr, 0, s);
 }
 
-// encoder transform (forward_prtr_fast, net:379-382) + quantize epilogue
-int run_enc(lbc_model* m, Work& w, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, hipStream_t s) {
+// encoder transform (forward_prtr_fast, net:379-382) + quantize epilogue.  part: 0 all, 1 the layers before the
+// quantising GEMM (they do not read the context net's output), 2 the quantising GEMM only
+int run_enc(lbc_model* m, Work& w, GemmArgs g, int32_t* sym, int32_t* idx, float* bits, hipStream_t s, int part = 0) {
     int rc;
     float *e0 = w.e0.as<float>(), *e1 = w.e1.as<float>();
+    const int W = m->NP;
+    if (part != 2) {
     {
         GemmArgs c = g;
         c.nseg = 0;
@@ -720,12 +743,13 @@ int run_enc(lbc_model* m, Work& w, GemmArgs g, int32_t* sym, int32_t* idx, float
         sx = Seg{c.geo.x, SEG_X, 0, 0, 0, 4 * m->Cx, 5 * m->Cx};
         if ((rc = gemm(c, s))) return rc;
     }
-    const int W = m->NP;
     if ((rc = run_gdn(g, m->net->g0, e0, W, false, e1, s))) return rc;
     if ((rc = run_dense(g, m->net->e1, e1, W, EPI_BIAS, e0, W, s))) return rc;
     if ((rc = run_gdn(g, m->net->g1, e0, W, false, e1, s))) return rc;
     if ((rc = run_dense(g, m->net->e2, e1, W, EPI_BIAS, e0, W, s))) return rc;
     if ((rc = run_gdn(g, m->net->g2, e0, W, false, e1, s))) return rc;
+    if (part == 1) return LBC_OK;
+    }
     GemmArgs c = g;
     c.ksi = w.ksi.as<float>();
     c.ldk = m->C4;
@@ -820,6 +844,9 @@ void lbc_destroy(lbc_model* m) {
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
     for (auto& kv : m->band_exec) (void)hipGraphExecDestroy(kv.second);
     if (m->cap) (void)hipStreamDestroy(m->cap);
+    if (m->cap2) (void)hipStreamDestroy(m->cap2);
+    for (auto e : m->fev)
+        if (e) (void)hipEventDestroy(e);
     delete m;
 }
 
@@ -948,17 +975,30 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         int crc = prof_range_begin(&m->prof, 0, m->cap);
         drop_recs(m->prof, 0);
         const int4* blocks = m->blocks_enc.as<int4>();
+        const bool fork = enc_fork_on() && m->prof.sample_every == 0;   // (timing stamps assume one chain)
         g_prof = &m->prof;
         for (size_t t = 0; t < m->step_off.size(); ++t)
             if (m->step_cnt[t] > m->lane[0].rows) crc = set_error(LBC_E_STATE, "encoder workspace too small");
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
             m->prof.step(m->prof.sample_every > 0 && (t % m->prof.sample_every) == 0);
             GemmArgs g = base_args(m, blocks + m->step_off[t], m->step_cnt[t], m->x_in.as<float>(), n_img, Hb, Wb);
-            if (!crc)
-                crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad,
-                              m->l0_on ? m->cells_enc.as<int4>() + m->cell_off[t] : nullptr, m->l0_on ? m->cell_cnt[t] : 0);
-            if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
-                                    m->bits_buf.as<float>(), m->cap);
+            const int4* cells = m->l0_on ? m->cells_enc.as<int4>() + m->cell_off[t] : nullptr;
+            const int ncells = m->l0_on ? m->cell_cnt[t] : 0;
+            if (fork) {
+                // fork: the context net on cap2, the transform's first layers on cap; join before quantising
+                if (!crc) crc = hip_rc(hipEventRecord(m->fev[0], m->cap));
+                if (!crc) crc = hip_rc(hipStreamWaitEvent(m->cap2, m->fev[0], 0));
+                if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap2, frame_pad, cells, ncells);
+                if (!crc) crc = hip_rc(hipEventRecord(m->fev[1], m->cap2));
+                if (!crc) crc = run_enc(m, m->lane[0], g, nullptr, nullptr, nullptr, m->cap, 1);
+                if (!crc) crc = hip_rc(hipStreamWaitEvent(m->cap, m->fev[1], 0));
+                if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
+                                        m->bits_buf.as<float>(), m->cap, 2);
+            } else {
+                if (!crc) crc = run_ctx(m, m->lane[0], g, false, m->cap, frame_pad, cells, ncells);
+                if (!crc) crc = run_enc(m, m->lane[0], g, m->sym_buf.as<int32_t>(), m->idx_buf.as<int32_t>(),
+                                        m->bits_buf.as<float>(), m->cap);
+            }
             if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
         }
         m->prof.active = false;
