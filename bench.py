@@ -88,6 +88,9 @@ def parse_args(argv=None):
     ap.add_argument("--team-groups", default="last-full", choices=("last-full", "first-full"),
                     help="when --steps is not a multiple of --team: the partial group is the first launch (last-full) "
                          "or the last one (first-full)")
+    ap.add_argument("--drain-wg-per-cu", type=int, default=1, choices=(1, 2),
+                    help="team schedule: workgroups per CU of the last decode launch, which runs after the last encode "
+                         "with the GPU otherwise idle (LBC_OPT_TEAM_WG_PER_CU)")
     ap.add_argument("--workers", type=int, default=4,
                     help="headline schedule: W workers, each (own handle + stream + thread) compressing, entropy coding "
                          "and decoding whole batches (0 = the encoder + --depth decoders pipeline)")
@@ -364,7 +367,11 @@ def main():
                             t0_ = time.perf_counter()
                             sts = [f_.result() for (_, _, f_) in pend]
                             with torch.cuda.stream(s_decs[0]):
-                                zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb)
+                                # the last launch runs with the encoder finished (two workgroups per CU measured slower:
+                                # profiles/r02_exp/team_two_per_cu.txt)
+                                last = gi == len(sizes)
+                                zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb,
+                                                      wg_per_cu=args.drain_wg_per_cu if last else 1)
                                 s_decs[0].synchronize()
                             with plock:
                                 ph["decode"] += time.perf_counter() - t0_

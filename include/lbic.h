@@ -87,6 +87,11 @@ int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, floa
  * large-M GEMM; above 80 KB one encoder workgroup per CU, which leaves room for a decoder running
  * concurrently on another stream (bench.py's two-stage pipeline).  Results are unchanged. */
 #define LBC_OPT_ENC_LDS_FLOOR 1
+/* LBC_OPT_TEAM_WG_PER_CU (1 or 2): workgroups per CU of the lbc_decode_team launches this handle leads (as the
+ * first handle of the call).  1 (default): a team of CUs/8 workgroups per batch, one per CU, leaving registers and
+ * LDS to an encoder running concurrently on another stream.  2: two per CU (teams of 2 * CUs/8), every register
+ * of the CU -- for a decode with the GPU otherwise idle (e.g. the last launch of a pipeline).  Results unchanged. */
+#define LBC_OPT_TEAM_WG_PER_CU 2
 int lbc_set_option(lbc_model *m, int option, long long value);
 
 /* lbc_encode with flags.  LBC_ENC_FRAME_PAD: the context net's layer-0 map is zero outside the frame

@@ -173,6 +173,7 @@ struct lbc_model {
     DevBuf l0, cells_enc;
     std::vector<int> cell_off, cell_cnt;
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
+    int team_wpc = 1;           // LBC_OPT_TEAM_WG_PER_CU
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -826,6 +827,10 @@ int lbc_set_option(lbc_model* m, int option, long long value) {
             if (value < 0 || value > 160 * 1024) return set_error(LBC_E_ARG, "LDS floor out of range [0, 160 KB]");
             m->enc_lds_floor = (int)value;
             return LBC_OK;
+        case LBC_OPT_TEAM_WG_PER_CU:
+            if (value < 1 || value > 2) return set_error(LBC_E_ARG, "team workgroups per CU must be 1 or 2");
+            m->team_wpc = (int)value;
+            return LBC_OK;
     }
     return set_error(LBC_E_ARG, "unknown option");
 }
@@ -1372,7 +1377,10 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     HIPCHK(hipSetDevice(dev));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_cu = team_blocks_per_cu();
-    int S = std::min(32, cus / TEAM_MAX);     // grid 8 x S: one XCD slot per team (k_dec_team)
+    // grid 8 x S: one XCD slot per team (k_dec_team); S = one (or, LBC_OPT_TEAM_WG_PER_CU, two) workgroups per CU
+    // of an XCD -- the whole grid must be resident (team barriers), so never more than the occupancy allows
+    const int wpc = std::min(m0->team_wpc, per_cu);
+    int S = std::min(32, cus / TEAM_MAX) * std::max(wpc, 1);
     if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
     if (S < 1 || per_cu < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     for (int t = 0; t < T; ++t) {

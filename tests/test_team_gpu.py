@@ -41,7 +41,7 @@ def batches(arch, T, n, Hb, Wb, seed, scale=0.5):
             for _ in range(T)]
 
 
-def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05):
+def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
     """Encode T batches, decode them by the graph decoder and by one team launch; return both."""
     from lbic.model import decompress_teams
     arch, hs = handles(name, T)
@@ -51,7 +51,7 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05):
     ref = [hs[0].decompress_batch(s, Hb, Wb) for s in st]
     for r, z in zip(rs, ref):
         assert torch.equal(r["zhat"], z)
-    got = decompress_teams(hs, st, Hb, Wb)
+    got = decompress_teams(hs, st, Hb, Wb, wg_per_cu=wpc)
     return ref, got, hs, st
 
 
@@ -86,6 +86,23 @@ def test_team_ragged_frames_ks3311(shape, monkeypatch):
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
     ref, got, _, _ = run_case("tiny_ks3311", 3, 2, *shape, seed=sum(shape))
     for t in range(3):
+        assert torch.equal(got[t], ref[t])
+
+
+@pytest.mark.parametrize("name,T,n,shape", [("b8_lowrate_2rows", 8, 32, (2, 96)), ("tiny_ks3311", 8, 3, None),
+                                            ("b8_lowrate_2rows", 3, 35, (2, 7))])
+def test_team_two_workgroups_per_cu(name, T, n, shape, monkeypatch):
+    """LBC_OPT_TEAM_WG_PER_CU = 2 (the launch with the GPU otherwise idle): teams of twice the workgroups, two per
+    CU, each workgroup half the output tiles -- the same results; then a one-per-CU launch on the same handles."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    g = load_golden("loop_" + name)
+    Hb, Wb = shape or g["x"].shape[:2]
+    ref, got, hs, st = run_case(name, T, n, Hb, Wb, seed=T + n, wpc=2)
+    for t in range(T):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    from lbic.model import decompress_teams
+    got = decompress_teams(hs, st, Hb, Wb, wg_per_cu=1)
+    for t in range(T):
         assert torch.equal(got[t], ref[t])
 
 
