@@ -143,8 +143,9 @@ int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, 
  * handle ms[t] (distinct handles of one geometry, e.g. lbc_create_sibling) from streams[t * n_img + i] /
  * lens[t * n_img + i] into zhat_devs[t]; results are bit-identical to lbc_decode of each batch.  All batches run
  * in ONE persistent GPU launch (k_dec_team: one team of workgroups per batch, team barriers between the operations
- * of a raster step).  Batches the team kernel does not cover (streams averaging >= 1 bit per symbol, M > 256) are
- * decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
+ * of a raster step).  The rANS operation picks its variant by rate as lbc_decode does: below 1 bit per symbol the
+ * sparse one, otherwise the dense one on a copy of the tables every workgroup stages in its LDS at launch start.
+ * Batches the team kernel does not cover (M > 256, buffers past 4 GB) are decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
 int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *streams, const size_t *lens, int n_img,
                     int Hb, int Wb, float *const *zhat_devs, void *stream);
 /* raw stamps of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 256 per team (team rank 0), s_memrealtime
@@ -157,6 +158,9 @@ int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, in
  * (per raster step, the graph decoder's accounting: weights + A rows + outputs once per GEMM, rANS inputs and
  * outputs; times teams x Hb x Wb) and whether it ran with plain hand-off stores (1) or write-through ones (0). */
 int lbc_team_stats(const lbc_model *m, double *launch_ms, double *bytes, double *flops, int *plain);
+/* how the last lbc_decode_team call led by m decoded: 0 lbc_decode per batch (fallback), 1 one team launch with the
+ * sparse rANS variant, 2 one team launch with the dense variant (tables in LDS). */
+int lbc_team_mode(const lbc_model *m, int *mode);
 
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder

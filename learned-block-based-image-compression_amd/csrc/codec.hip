@@ -205,6 +205,7 @@ struct lbc_model {
     TeamArgs team_args{};
     std::vector<unsigned long long> team_ts_host;
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
+    int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
 };
@@ -1333,11 +1334,12 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
 // The raster step each team replays is recorded from the same run_ctx / run_dec calls that build the graph decoder
 // (three column classes: the KS3311 layer-0 cache computes border cells at h = 0 and h = Wb - 1), so the team
 // decoder computes exactly what lbc_decode computes.  Falls back to lbc_decode per batch where the team kernel does
-// not apply (dense rANS tables, M > 256, buffers past the 4 GB reach of its buffer loads, LBIC_TEAM=0).
+// not apply (M > 256, buffers past the 4 GB reach of its buffer loads, LBIC_TEAM=0, an LDS image past 160 KB).
 static std::mutex g_team_mu;   // one team launch at a time per process: its grid must be resident as a whole
 
 static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* streams, const size_t* lens, int n_img,
                          int Hb, int Wb, float* const* zhat, void* stream) {
+    ms[0]->team_mode_last = 0;
     for (int t = 0; t < T; ++t) {
         const int rc = lbc_decode(ms[t], streams + (size_t)t * n_img, lens + (size_t)t * n_img, n_img, Hb, Wb, zhat[t],
                                   stream);
@@ -1367,7 +1369,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     const int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
     const double zbytes = (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->Cx * 4;
     const double lbytes = ms[0]->l0_on ? (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->C1P * 4 : 0.0;
-    if ((te && atoi(te) == 0) || !sparse || ms[0]->M > 256 || zbytes >= 4294967296.0 || lbytes >= 4294967296.0)
+    if ((te && atoi(te) == 0) || ms[0]->M > 256 || zbytes >= 4294967296.0 || lbytes >= 4294967296.0)
         return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     std::lock_guard<std::mutex> team_lock(g_team_mu);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1438,7 +1440,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
             r.ksi = w.ksi.as<float>();
             r.yq = w.yq.as<float>();
             r.rows = n_img;
-            r.sparse = 1;
+            r.sparse = sparse;
             rans.push_back(r);
         }
         const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
@@ -1461,6 +1463,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.sync = m0->team_sync.as<unsigned>();
         // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
         a.ni_max = 2;
+        a.tab16 = rans[0].total16;
         for (const GemmArgs& d : gem) {
             const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
             if (team_fast_path(d, S)) a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
@@ -1496,6 +1499,8 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         m0->team_key = key;
     }
     TeamArgs a = m0->team_args;
+    a.dense = sparse ? 0 : 1;   // high rates: the tables staged in every workgroup's LDS (rans_row<true>)
+    if (team_lds_bytes(a) > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     a.tmo = 100000000ull;                    // 1 s at one barrier: far above any operation's time
     const char* st = getenv("LBIC_TEAM_STAMPS");
     a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
@@ -1527,6 +1532,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         m0->team_fallbacks += 1;
     }
     m0->team_plain_last = a.plain;
+    m0->team_mode_last = a.dense ? 2 : 1;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
     m0->dec_timed = true;
@@ -1554,6 +1560,12 @@ int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double*
     *bytes = m->team_launch_bytes;
     *flops = m->team_launch_flops;
     *plain = m->team_plain_last;
+    return LBC_OK;
+}
+
+int lbc_team_mode(const lbc_model* m, int* mode) {
+    if (!m || !mode) return set_error(LBC_E_ARG, "null argument");
+    *mode = m->team_mode_last;
     return LBC_OK;
 }
 

@@ -111,7 +111,7 @@ constexpr int TEAM_NI_MAX = 6;     // output tiles per workgroup and GEMM on the
 struct TeamArgs {
     const GemmArgs* gemm;    // [T][3][NG] prepared GEMMs of one raster step, per team and column class
                              // (0: h = 0, 1: 0 < h < Wb - 1, 2: h = Wb - 1); block rows / columns set in-kernel
-    const RansArgs* rans;    // [T] (sparse decoder, one stream per image)
+    const RansArgs* rans;    // [T] (one stream per image)
     int opk[TEAM_MAXOPS];    // the step: >= 0 a GEMM index, -1 the rANS decode
     int nops, NG, T, S, Hb, Wb;
     unsigned* sync;          // [T][32]: per team [0] arrival counter, [1] XCD census (one 128-byte line each), then
@@ -127,6 +127,10 @@ struct TeamArgs {
     int sv, sh;
     int pf;                  // weight tiles of the NEXT operation each workgroup requests while it waits at a team
                              // barrier (0 = none): they arrive in the team's L2 before the operation starts
+    int dense;               // 1: the streams average >= 1 bit per symbol (high rates): every workgroup stages the
+                             // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>
+                             // on them; 0: rans_row_sparse (centre intervals, tables from global memory)
+    int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
@@ -136,6 +140,7 @@ __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
 }
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
+size_t team_lds_bytes(const TeamArgs& a);   // k_dec_team's dynamic LDS for a launch
 int launch_dec_team(const TeamArgs& a, hipStream_t s);
 int team_blocks_per_cu();          // k_dec_team workgroups one CU holds (occupancy query; 0 on error)
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm

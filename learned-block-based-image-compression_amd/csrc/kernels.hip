@@ -383,194 +383,6 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     }
 }
 
-// ----------------------------------------------------------------------------------------- rANS decode
-// One 64-lane wave per stream (reference format: one per image) decodes the Mlat symbols of the current
-// block (RansDecoder::decode_stream, called per block at net:439), entirely on the GPU.  Up to 8 streams
-// share a workgroup and one LDS copy of the tables (build_rans_gpu_tables: CDF entries stored as c - 1,
-// a 64-entry coarse row per table, fine rows padded with 0xFFFF).  The 64-bit state is wave-uniform
-// (SGPRs); one wave issues about one instruction per 4 cycles, so the per-symbol body is kept short and
-// everything that does not depend on the state is done a symbol ahead:
-//   * before the loop, every lane gathers the table metadata of "its" symbols (lane i of chunk kb =
-//     symbol 64 kb + i); per symbol the next symbol's metadata is a v_readlane and its coarse row an
-//     LDS read issued while the current symbol waits for its own fine read;
-//   * level 1: cum against the prefetched coarse row (one compare + popcount) picks a segment of S
-//     symbols; level 2: one 64-wide LDS window read from that segment start, compare + popcount gives
-//     the symbol, two v_readlanes its interval (a short table, <= 64 entries, has S = 1);
-//   * the block's stream words are staged in LDS with the tables; renormalisation takes the next word
-//     from there, requested as soon as the previous one is consumed.
-// Output: y_qnt = sym + mean (dequantize, entropy_layers_cai.py:159-168, net:440-442).
-// Called by every wave of the workgroup (rows past a.rows only help fill the LDS tables): the wave's
-// stream state and indexes are requested first, the workgroup then copies the tables into LDS while those
-// loads are in flight.
-__device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int row_in, int lane) {
-    RSTAMP(0);
-    const bool valid = row_in < a.rows;
-    const int row = valid ? row_in : a.rows - 1;
-    // stream / state of this row: the image's (reference format: row = image) or the block row's
-    // (sub-stream format, via the block list)
-    int img = row;
-    if (a.streams_per_img > 1) {
-        const int4* blocks = a.ctr ? a.blocks + (long)(*a.ctr) * a.ctr_stride : a.blocks;
-        const int4 blk = blocks[row];
-        img = blk.x * a.streams_per_img + blk.y;
-    }
-    img = __builtin_amdgcn_readfirstlane(img);
-    const int Mlat = a.Mlat;
-    // per-table metadata, lane t holds table t
-    const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
-    const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane];
-    const unsigned long long x_in = a.state_x[img];
-    const int p_in = a.state_ptr[img];
-    const long long wb = a.word_base[img];
-    const int nw_in = a.word_count[img];
-    // table of symbol i (ti) and of symbol i + 1 (tn: the next symbol's metadata is read a symbol ahead)
-    int ti[4], tn[4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int i = kb * 64 + lane;
-        // clamped, unconditional loads (indexes are 0..63 by construction; entries past Mlat are unused)
-        ti[kb] = a.idx[(long)row * Mlat + min(i, Mlat - 1)] & 63;
-        tn[kb] = a.idx[(long)row * Mlat + min(i + 1, Mlat - 1)] & 63;
-    }
-    // LDS staging: the tables (one image built on the host) and this wave's stream words p0 .. p0 +
-    // RANS_WIN - 1 (0 past the stream's end; a block never needs more: <= 52 bits per symbol incl. a
-    // bypass escape), so renormalisation reads LDS at a uniform address instead of global memory.  The
-    // first table chunk is requested before anything waits (it depends on nothing), the words as soon as
-    // the stream position has arrived; loads are clamped and unconditional and all issued before the
-    // first LDS store (a guarded load, or a load -> store pair per iteration, waits for each in turn).
-    const uint4* tsrc = reinterpret_cast<const uint4*>(a.cdf16);
-    uint4* tdst = reinterpret_cast<uint4*>(lds);
-    const int n16 = a.total16 / 8, bd = blockDim.x;
-    uint4 r[RANS_FILL];
-#pragma unroll
-    for (int k = 0; k < RANS_FILL; ++k) r[k] = tsrc[min((int)threadIdx.x + k * bd, n16 - 1)];
-    unsigned long long x = uni64(x_in);
-    int p = __builtin_amdgcn_readfirstlane(p_in);
-    const uint32_t* w = a.words + wb;
-    const int nw = __builtin_amdgcn_readfirstlane(nw_in);
-    const int p0 = p;
-    {
-        uint32_t* win = reinterpret_cast<uint32_t*>(lds + a.total16) + (threadIdx.x >> 6) * RANS_WIN;
-        uint32_t wv[RANS_WIN / 64];
-#pragma unroll
-        for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
-#pragma unroll
-        for (int k = 0; k < RANS_FILL; ++k) tdst[min((int)threadIdx.x + k * bd, n16 - 1)] = r[k];   // past the end: a duplicate
-        for (int i0 = threadIdx.x + RANS_FILL * bd; i0 < n16; i0 += RANS_FILL * bd) {   // tables > RANS_FILL chunks
-#pragma unroll
-            for (int k = 0; k < RANS_FILL; ++k) r[k] = tsrc[min(i0 + k * bd, n16 - 1)];
-#pragma unroll
-            for (int k = 0; k < RANS_FILL; ++k) tdst[min(i0 + k * bd, n16 - 1)] = r[k];
-        }
-#pragma unroll
-        for (int k = 0; k < RANS_WIN / 64; ++k) win[k * 64 + lane] = p0 + k * 64 + lane < nw ? wv[k] : 0u;
-    }
-    // symbol-major metadata (gathered from the table lanes): lane i of chunk kb = symbol 64 kb + i + 1
-    // (fine row start, S, escape symbol, coarse row start); the offset of symbol 64 kb + i itself
-    int nfbv[4], nSv[4], nlmv[4], ncav[4], moff[4], symv[4];
-    int fb, S, lm2, ca0;
-    {
-        const int sel0 = __builtin_amdgcn_readfirstlane(ti[0]);
-        fb = rdlane_i(t_fb, sel0); S = rdlane_i(t_S, sel0); lm2 = rdlane_i(t_lm2, sel0); ca0 = rdlane_i(t_ca, sel0);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int sel = tn[kb] << 2;
-        nfbv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_fb);
-        nSv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_S);
-        nlmv[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lm2);
-        ncav[kb] = __builtin_amdgcn_ds_bpermute(sel, t_ca);
-        moff[kb] = __builtin_amdgcn_ds_bpermute(ti[kb] << 2, t_off);
-        symv[kb] = 0;
-    }
-    __syncthreads();
-    if (!valid) return;
-    RSTAMP(1);
-    int bad = 0;
-    const uint32_t* win = reinterpret_cast<const uint32_t*>(lds + a.total16) + (threadIdx.x >> 6) * RANS_WIN;
-    // words q0 .. q0 + 63 of the LDS window lane-distributed in a register; wn = the word renormalisation
-    // takes next (a v_readlane, prepared as soon as the previous word is consumed)
-    int q0 = 0;
-    uint32_t wbuf = win[lane];
-    uint32_t wn = rdlane(wbuf, 0);
-    auto renorm = [&]() {
-        uint32_t t = (uint32_t)(x >> 32) | ((uint32_t)x >> 31);   // 0 <=> x < RANS64_L = 2^31
-        asm("" : "+s"(t));               // keep the test on the scalar unit (not a 64-bit VALU compare)
-        if (t == 0) {
-            x = (x << 32) | wn;
-            ++p;
-            if (p - p0 - q0 >= 64) {     // next 64 words (rare: a stall of one LDS read)
-                q0 = min(q0 + 64, RANS_WIN - 64);
-                wbuf = win[q0 + lane];
-            }
-            wn = rdlane(wbuf, min(p - p0 - q0, 63));
-        }
-        x = uni64(x);
-    };
-    const char* lb = reinterpret_cast<const char*>(lds);
-    const int lane2 = lane * 2;
-    uint32_t cv = *reinterpret_cast<const uint16_t*>(lb + ca0 + lane2);   // coarse row of symbol 0
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int cnt_i = __builtin_amdgcn_readfirstlane(min(64, Mlat - kb * 64));
-        if (cnt_i <= 0) break;
-        for (int ii = 0; ii < cnt_i; ++ii) {
-            const uint32_t cum = (uint32_t)x & 0xffffu;
-            // level 1: segment j (coarse lane 0 is never counted: j = #entries <= cum, minus one)
-            const int j = __popcll(__ballot(cv < cum));
-            const int sbb = j * S;                  // segment start (bytes; fb and S are in bytes)
-            const uint32_t fine = *reinterpret_cast<const uint16_t*>(lb + fb + sbb + lane2);
-            // next symbol's metadata and coarse row, in the shadow of the fine read
-            const int nfb = rdlane_i(nfbv[kb], ii), nS = rdlane_i(nSv[kb], ii);
-            const int nlm2 = rdlane_i(nlmv[kb], ii), nca = rdlane_i(ncav[kb], ii);
-            const uint32_t cvn = *reinterpret_cast<const uint16_t*>(lb + nca + lane2);
-            __builtin_amdgcn_sched_barrier(0);   // both LDS reads issued before the fine read is waited for
-            // level 2: the window from the segment start (lane 0 is <= cum by construction; a short
-            // table has S = 1, so its window always answers kk = 0)
-            const int kk = __popcll(__ballot(fine < cum) | 1ull) - 1;
-            const int s = (sbb >> 1) + kk;
-            const uint32_t start = (rdlane(fine, kk) + 1u) & 0xffffu;   // e + 1 = c (the c = 0 entry wraps)
-            const uint32_t nxt = rdlane(fine, kk + 1) + 1u;
-            x = (unsigned long long)(nxt - start) * (x >> 16) + (cum - start);
-            renorm();
-            int v = s;
-            if (__builtin_expect(s == lm2, 0)) {   // escape: value coded in 4-bit bypass chunks
-                auto get_bits = [&]() -> uint32_t {
-                    const uint32_t b = (uint32_t)(x & 15u);
-                    x >>= 4;
-                    renorm();
-                    return b;
-                };
-                uint32_t cc = get_bits(), nb = cc;
-                while (cc == 15u && nb <= 8) { cc = get_bits(); nb += cc; }
-                if (nb > 8) { bad |= 4; nb = 0; }
-                uint32_t raw = 0;
-                for (uint32_t jj = 0; jj < nb; ++jj) raw |= get_bits() << (jj * 4);
-                v = (int)(raw >> 1);
-                v = (raw & 1) ? -v - 1 : v + lm2;
-            }
-            symv[kb] = lane == ii ? v : symv[kb];
-            fb = nfb; S = nS; lm2 = nlm2; cv = cvn;
-        }
-    }
-    RSTAMP(2);
-    bad |= p > nw;                       // consumed words past the end of the stream
-    bad |= (p - p0 > RANS_WIN) ? 8 : 0;  // (cannot happen: <= 52 bits per symbol)
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-        const int i = kb * 64 + lane;
-        if (i < Mlat) {
-            if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
-            else a.yq[(long)row * a.ldy + i] = (float)(symv[kb] + moff[kb]) + a.ksi[(long)row * a.ldk + Mlat + i];
-        }
-    }
-    if (lane == 0) {
-        a.state_x[img] = x;
-        a.state_ptr[img] = p;
-        if (bad) a.status[img] = bad;
-    }
-    RSTAMP(3);
-}
 
 __global__ __launch_bounds__(RANS_WPB * 64) void k_rans_decode(const RansArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcdf[];

@@ -318,10 +318,14 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // hand-off: values are stored plain (they stay in that L2) and still loaded sc1 (past the reading CU's L1).  If
 // any team of the launch spans XCDs the launch stops before its first operation with failure word 2 and the host
 // relaunches with plain = 0 (every hand-off write-through): results never depend on placement.
-// 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch
+// 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch.
+// DENSE (TeamArgs::dense): the high-rate instance, tables staged in LDS and rans_row<true>; a separate instance so the
+// low-rate one keeps its register allocation.
+template <bool DENSE>
 __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
     // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
+    // [dense rANS only: the table image, total16 16-bit entries]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
     uint32_t* lwin = team_lds;
     int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN);
@@ -336,6 +340,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(red + ta.ni_max * KSPLIT * 256);
     // the recorded operations are read-only for the launch: constant address space, so their fields come in by
     // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
     typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
@@ -344,6 +349,12 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
     unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 256 : nullptr;
     if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
+    if (DENSE) {     // the rANS tables, once per launch (read-only: no hand-off); the census barrier's
+        const uint4* src = reinterpret_cast<const uint4*>(R.cdf16);      // __syncthreads (or the one below) orders them
+        uint4* dst = reinterpret_cast<uint4*>(tab);
+        for (int i = threadIdx.x; i < R.total16 / 8; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
     unsigned target = 0;
     const bool wt = !ta.plain;
     if (ta.plain) {
@@ -374,7 +385,10 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
                     if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
-                        for (int r = rank; r < R.rows; r += S) rans_row_sparse<true>(R, lwin, r, lane, wt);
+                        for (int r = rank; r < R.rows; r += S) {
+                            if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
+                            else rans_row_sparse<true>(R, lwin, r, lane, wt);
+                        }
                     } else if (ta.split_op >= 0) {
                         team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]), v, h, rank, S, red,
                                       wt, 1, ta.split_wy);
@@ -404,10 +418,14 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
 
 int team_blocks_per_cu() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team), 512, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team<false>), 512, 0) !=
         hipSuccess)
         return 0;
     return nb;
+}
+
+size_t team_lds_bytes(const TeamArgs& a) {
+    return (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)a.dense * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
@@ -415,13 +433,15 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
         return set_error(LBC_E_ARG, "bad team decoder arguments");
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
     static const bool attr = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_team), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        for (const void* f : {reinterpret_cast<const void*>(&k_dec_team<false>), reinterpret_cast<const void*>(&k_dec_team<true>)})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
-    const size_t lds = (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4;
-    hipLaunchKernelGGL(k_dec_team, dim3(8 * a.S), dim3(512), lds, s, a);
+    const size_t lds = team_lds_bytes(a);
+    if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
+    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, dim3(8 * a.S), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_team<false>, dim3(8 * a.S), dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

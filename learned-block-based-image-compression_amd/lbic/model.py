@@ -242,11 +242,15 @@ class BlockBasedImgCompLossyNetv9:
 
     def team_stats(self):
         """The last decompress_teams launch led by this handle (lbc_team_stats): dict(launch_ms, bytes, flops,
-        plain) -- its duration, algorithmic bytes / FLOPs, and the hand-off store mode it ran in."""
+        plain, mode) -- its duration, algorithmic bytes / FLOPs, the hand-off store mode it ran in, and how the call
+        decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant, or "fallback" to lbc_decode per batch)."""
         L = _lib.lib()
         ms, by, fl, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         _lib.check(L.lbc_team_stats(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(fl), ctypes.byref(pl)))
-        return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value)
+        mode = ctypes.c_int()
+        _lib.check(L.lbc_team_mode(self._h, ctypes.byref(mode)))
+        return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value,
+                    mode=("fallback", "team_sparse", "team_dense")[mode.value])
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]

@@ -3,7 +3,7 @@ workgroups per batch, must reproduce the graph decoder (lbc_decode, itself bit-e
 reference's closed loops in test_gpu_parity.py) bit for bit: every geometry class of the recorded raster step
 (KS3111, KS3311 with the layer-0 cache's border classes), ragged frames, image counts that do not fill a 16-row
 tile or need three row tiles, tiny teams (many output tiles per workgroup: the weight-prefetch loop), corrupt
-streams, and the fallback for streams the team kernel does not take."""
+streams, both rANS variants (sparse at low rates, dense with the tables in LDS at high rates), and the fallback."""
 import types
 
 import numpy as np
@@ -117,14 +117,39 @@ def test_team_small_teams(S, monkeypatch):
         assert torch.equal(got[t], ref[t])
 
 
+@pytest.mark.parametrize("name,T,n,shape,scale", [
+    ("tiny_ks3111", 3, 5, None, 0.05), ("tiny_ks3311", 8, 3, None, 0.05), ("b8_lowrate_2rows", 4, 32, (2, 24), 0.05),
+    ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
+def test_team_dense_rans(name, T, n, shape, scale, monkeypatch):
+    """The dense rANS variant inside the team kernel (high rates; every workgroup stages the tables in its LDS once per
+    launch, one wave per stream runs rans_row<true>): forced by LBIC_RANS_SPARSE=0 at the fixtures' low rates, and
+    picked by rate (>= 1 bit per symbol, bypass escapes included) on high-amplitude batches."""
+    if scale < 1:
+        monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
+    else:
+        monkeypatch.delenv("LBIC_RANS_SPARSE", raising=False)
+    g = load_golden("loop_" + name)
+    Hb, Wb = shape or g["x"].shape[:2]
+    ref, got, hs, st = run_case(name, T, n, Hb, Wb, seed=T * 5 + n, scale=scale)
+    nsym = T * n * Hb * Wb * golden_arch(g).M
+    for t in range(T):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    if scale >= 1:
+        bits = 8.0 * sum(len(s) for b in st for s in b)
+        assert bits / nsym >= 1.0, f"high-amplitude batch coded at {bits / nsym:.3f} bits per symbol"
+    assert hs[0].team_stats()["mode"] == "team_dense"
+
+
 def test_team_fallback_and_errors(monkeypatch):
-    """Streams the team kernel does not take (dense rANS variant, LBIC_TEAM=0) decode through lbc_decode with the
-    same results; a truncated stream raises; the handles work afterwards."""
+    """LBIC_TEAM=0: the batches decode through lbc_decode one after another with the same results; a truncated stream
+    raises; the handles work afterwards."""
     from lbic.model import decompress_teams
-    monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
+    monkeypatch.setenv("LBIC_TEAM", "0")
     ref, got, hs, st = run_case("tiny_ks3111", 2, 3, 4, 5, seed=3)
     for t in range(2):
         assert torch.equal(got[t], ref[t])
+    assert hs[0].team_stats()["mode"] == "fallback"
+    monkeypatch.delenv("LBIC_TEAM")
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
     bad = [list(st[0]), list(st[1])]
     bad[1][2] = bad[1][2][:8]
@@ -135,6 +160,7 @@ def test_team_fallback_and_errors(monkeypatch):
     got = decompress_teams(hs, st, 4, 5)
     for t in range(2):
         assert torch.equal(got[t], ref[t])
+    assert hs[0].team_stats()["mode"] == "team_sparse"
 
 
 def test_team_stamps(monkeypatch):
