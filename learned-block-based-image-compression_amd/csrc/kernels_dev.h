@@ -26,13 +26,13 @@ __device__ __forceinline__ void warm_kernargs() {
     if constexpr (NLINES <= 3) {
         asm volatile("s_load_dword %0, %3, 0x0\n\ts_load_dword %1, %3, 0x40\n\ts_load_dword %2, %3, 0x80\n\t"
                      "s_waitcnt lgkmcnt(0)"
-                     : "=s"(d0), "=s"(d1), "=s"(d2) : "s"(kp) : "memory");
+                     : "=&s"(d0), "=&s"(d1), "=&s"(d2) : "s"(kp) : "memory");
     } else {
         asm volatile("s_load_dword %0, %10, 0x0\n\ts_load_dword %1, %10, 0x40\n\ts_load_dword %2, %10, 0x80\n\t"
                      "s_load_dword %3, %10, 0xc0\n\ts_load_dword %4, %10, 0x100\n\ts_load_dword %5, %10, 0x140\n\t"
                      "s_load_dword %6, %10, 0x180\n\ts_load_dword %7, %10, 0x1c0\n\ts_load_dword %8, %10, 0x200\n\t"
                      "s_load_dword %9, %10, 0x230\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(d0), "=s"(d1), "=s"(d2), "=s"(d3), "=s"(d4), "=s"(d5), "=s"(d6), "=s"(d7), "=s"(d8), "=s"(d9)
+                     : "=&s"(d0), "=&s"(d1), "=&s"(d2), "=&s"(d3), "=&s"(d4), "=&s"(d5), "=&s"(d6), "=&s"(d7), "=&s"(d8), "=&s"(d9)
                      : "s"(kp) : "memory");
     }
 }
