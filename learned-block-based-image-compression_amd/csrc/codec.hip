@@ -1384,6 +1384,11 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     const int wpc = std::min(m0->team_wpc, per_cu);
     int S = std::min(32, cus / TEAM_MAX) * std::max(wpc, 1);
     if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
+    // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches alone:
+    // 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD per team
+    const char* spe = getenv("LBIC_TEAM_SPREAD");
+    const int spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
+    S *= spread;
     if (S < 1 || per_cu < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     for (int t = 0; t < T; ++t) {
         lbc_model* m = ms[t];
@@ -1395,7 +1400,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         if ((rc = upload_streams(m, subs, s))) return rc;
     }
     // the recorded program, rebuilt when any team's buffers or weights moved
-    std::vector<long long> key = {T, S, n_img, Hb, Wb};
+    std::vector<long long> key = {T, S, spread, n_img, Hb, Wb};
     for (int t = 0; t < T; ++t) {
         lbc_model* m = ms[t];
         for (long long x : {(long long)m->words.p, (long long)m->zpad.p, (long long)m->lane[0].ctx0.p,
@@ -1458,6 +1463,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.NG = NG;
         a.T = T;
         a.S = S;
+        a.spread = spread;
         a.Hb = Hb;
         a.Wb = Wb;
         a.sync = m0->team_sync.as<unsigned>();
@@ -1517,7 +1523,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     // plain hand-off stores unless LBIC_TEAM_SC1=1; a launch that finds a team spread over XCDs stops before its
     // first operation (failure word 2, nothing decoded yet) and is rerun with write-through hand-offs
     const char* sc1e = getenv("LBIC_TEAM_SC1");
-    a.plain = sc1e && atoi(sc1e) ? 0 : 1;
+    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 ? 0 : 1;
     unsigned fail = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));

@@ -131,6 +131,8 @@ struct TeamArgs {
                              // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>
                              // on them; 0: rans_row_sparse (centre intervals, tables from global memory)
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
+    int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
+                             // ranks over two XCDs; hand-offs write-through, plain = 0)
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {

@@ -334,7 +334,10 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
-    const int team = blockIdx.x & 7, rank = blockIdx.x >> 3;
+    // spread 2 (at most four teams): team t = the workgroups of slots 2t and 2t + 1 (two XCDs), ranks interleaved
+    const int slot = blockIdx.x & 7;
+    const int team = ta.spread == 2 ? slot >> 1 : slot;
+    const int rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
     if (team >= T || rank >= S) return;
     unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
@@ -440,8 +443,11 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     (void)attr;
     const size_t lds = team_lds_bytes(a);
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
-    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, dim3(8 * a.S), dim3(512), lds, s, a);
-    else hipLaunchKernelGGL(k_dec_team<false>, dim3(8 * a.S), dim3(512), lds, s, a);
+    if (a.spread != 1 && (a.spread != 2 || a.T > TEAM_MAX / 2 || a.S % 2 || a.plain))
+        return set_error(LBC_E_ARG, "bad team spread");
+    const dim3 grid(8 * a.S / a.spread);
+    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_team<false>, grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

@@ -106,6 +106,22 @@ def test_team_two_workgroups_per_cu(name, T, n, shape, monkeypatch):
         assert torch.equal(got[t], ref[t])
 
 
+@pytest.mark.parametrize("spread", [1, 2])
+@pytest.mark.parametrize("name,T,n,shape", [("b8_lowrate_2rows", 4, 32, (2, 24)), ("tiny_ks3311", 3, 5, (3, 4)),
+                                            ("b8_lowrate_2rows", 1, 35, (2, 7))])
+def test_team_spread_two_xcds(name, T, n, shape, spread, monkeypatch):
+    """At most four batches: by default each team takes the workgroups of two XCD slots (twice the ranks,
+    write-through hand-offs); LBIC_TEAM_SPREAD=1 keeps one XCD per team (plain hand-offs) -- the same results as the
+    graph decoder either way."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_SPREAD", str(spread))
+    ref, got, hs, _ = run_case(name, T, n, *shape, seed=T + 2 * n)
+    for t in range(T):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    st = hs[0].team_stats()
+    assert st["mode"] == "team_sparse" and st["plain"] == (0 if spread == 2 else 1)
+
+
 @pytest.mark.parametrize("S", [1, 3, 7])
 def test_team_small_teams(S, monkeypatch):
     """Teams of 1, 3 and 7 workgroups: every workgroup walks many output tiles per GEMM (the weight-prefetch loop,
