@@ -149,6 +149,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
         }
     }
+    dstamp(dts, 5, 0.f);
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
@@ -175,10 +176,12 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             if (j == ni - 1) dstamp(dts, 3, acc[0]);
         };
         issue(0, w0);
+        dstamp(dts, 6, 0.f);
         {
             const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
             SRow rw;
             small_offsets(g, bk, lane, rw);
+            dstamp(dts, 7, 0.f);
 #pragma unroll
             for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
         }

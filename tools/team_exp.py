@@ -75,7 +75,7 @@ def main():
                               op_us_mean=[round(float(np.mean([o[k] for o in ops])), 2) for k in range(12)],
                               work_us_team0=comp[0], sc1=os.environ.get("LBIC_TEAM_SC1", "0"),
                               intra_cycles_team0=[[ts[0][64 + 8 * k + p] - ts[0][64 + 8 * k] if ts[0][64 + 8 * k + p] else 0
-                                                   for p in range(1, 5)] for k in range(12)])),
+                                                   for p in range(1, 8)] for k in range(12)])),
               flush=True)
 
 
