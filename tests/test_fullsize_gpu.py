@@ -153,3 +153,42 @@ def test_gang_past_int32_offsets():
     del r["symbols"], r["indexes"]
     z = m.decompress_batch(streams, Hb, Wb)
     assert torch.equal(z, r["zhat"]), "gang decode differs from the encoder's reconstruction"
+
+
+TEAM_FULL = {   # (arch, H, W, batches, frames per batch, rate): every config's frame size through the team decoder
+    "B8_lowrate": ((8, (3, 1, 1, 1), 768, 96), 768, 768, 8, 32, "low"),      # the headline's 8-batch launch
+    "B8_highrate": ((8, (3, 3, 1, 1), 1152, 128), 512, 768, 3, 3, "high"),
+    "B4_highrate": ((4, (3, 3, 1, 1), 512, 96), 768, 768, 2, 2, "high"),
+    "B16_lowrate": ((16, (3, 1, 1, 1), 1280, 192), 2048, 2048, 2, 2, "low"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TEAM_FULL))
+def test_team_full_size_roundtrip(name):
+    """lbc_decode_team at every config's real frame size (the headline's shape: 8 batches of 32 768x768 frames in
+    one launch): every batch decodes bit-exactly to the encoder's reconstruction, with the rANS variant the rate
+    calls for (sparse below 1 bit per symbol, the dense one with its tables in LDS above)."""
+    from lbic.arch import Arch
+    from lbic.model import decompress_teams
+    (B, KS, N, M), H, W, T, n, rate = TEAM_FULL[name]
+    arch = Arch(B, KS, N, M)
+    m = _model(arch, synth_state_dict(arch, 1337, rate=rate))
+    hs = [m] + [m.sibling() for _ in range(T - 1)]
+    Hb, Wb = H // B, W // B
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    zs, sts, nbytes = [], [], 0
+    for t in range(T):
+        x = torch.randint(0, 256, (n, Hb, Wb, arch.cx), generator=gen, device="cuda", dtype=torch.uint8)
+        r = m.compress_batch(x.float().div_(255.0).sub_(0.5))
+        st = m.entropy_encode(r["symbols"], r["indexes"])
+        nbytes += sum(len(s) for s in st)
+        zs.append(r["zhat"])
+        sts.append(st)
+        del x, r
+    got = decompress_teams(hs, sts, Hb, Wb)
+    for t in range(T):
+        assert torch.equal(got[t], zs[t]), f"{name} batch {t}: {(got[t] != zs[t]).sum().item()} values differ"
+    bps = 8.0 * nbytes / (T * n * Hb * Wb * M)
+    mode = hs[0].team_stats()["mode"]
+    print(f"{name} {T} x {n} x {H}x{W}: {bps:.3f} bits per symbol, {mode}")
+    assert mode == ("team_sparse" if bps < 1.0 else "team_dense")
