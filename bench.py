@@ -578,9 +578,11 @@ def main():
     rec = rec.cpu().numpy()
     bpp = float(np.mean(rec[:, 0] * 8.0 / (H * W)))
     psnr = float(np.mean(-10 * np.log10(rec[:, 1] / rec[:, 2])))
-    vs_ref = None
+    vs_ref = tq = None
     if rank == 0:
         vs_ref = compare_full_frame_fixture(enc_model, args, arch, dev)
+        if args.side_steps > 0:
+            tq = transform_quality(arch, cfg, dev, H, W)
 
     if rank != 0:
         if dist:
@@ -630,7 +632,7 @@ def main():
                      "included"},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"rate_point": args.rate, "bpp": round(bpp, 5), "psnr_db": round(psnr, 3),
-                    "enc_dec_bit_exact": bit_exact, "vs_ref": vs_ref},
+                    "enc_dec_bit_exact": bit_exact, "vs_ref": vs_ref, "transform_point": tq},
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
         "step_algorithmic_tflop": round(step_flops / 1e12, 3),
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
@@ -724,6 +726,37 @@ def roofline(kstats, dt, team=None, enc=None):
                 frac_of_span=round((fl / (kernels[dom]["avg_span_us"] * 1e-6) / 1e12 / peak) if bound == "mfma" else
                                    (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5))
     return roof, kernels
+
+
+def transform_quality(arch, cfg, dev, H, W, n=4):
+    """Quality at a working operating point (outside the timed region): the network with transform-codec weights
+    (lbic.weights.transform_state_dict: block DCT, frequency-weighted steps, no prediction) codes n structured
+    synthetic frames (smooth_frame) through the same library path -- compress, host rANS, GPU decode.  The
+    headline's weights are random at the config's rate, so its own PSNR carries no information; this one does."""
+    import numpy as np
+    import torch
+    from lbic.layout import image_to_blocks
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    from lbic.weights import TRANSFORM_STEP, smooth_frame, transform_state_dict
+    try:
+        sd = transform_state_dict(arch)
+    except ValueError as e:
+        return {"skipped": str(e)}
+    m = BlockBasedImgCompLossyNetv9(cfg, device=dev)
+    m.load_state_dict(sd)
+    m.update(force=True)
+    xb = torch.from_numpy(np.stack([image_to_blocks(smooth_frame(100 + i, H, W).astype(np.float32) / 255.0 - 0.5,
+                                                    arch.B) for i in range(n)])).to(dev)
+    r = m.compress_batch(xb)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    z = m.decompress_batch(st, H // arch.B, W // arch.B)
+    mse = ((z - xb) ** 2).double().mean(dim=(1, 2, 3)).cpu().numpy()
+    out = {"weights": f"transform_state_dict (block DCT, step {TRANSFORM_STEP}, {arch.M} coefficients)",
+           "frames": f"{n} smooth_frame synthetic {H}x{W}",
+           "bpp": round(float(np.mean([len(s) * 8.0 / (H * W) for s in st])), 5),
+           "psnr_db": round(float(np.mean(-10 * np.log10(mse))), 3),
+           "enc_dec_bit_exact": bool(torch.equal(z, r["zhat"]))}
+    return out
 
 
 def compare_full_frame_fixture(model, args, arch, dev):

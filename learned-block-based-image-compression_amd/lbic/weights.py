@@ -97,3 +97,94 @@ def load_reference_checkpoint(path: str) -> Dict[str, np.ndarray]:
     ck = torch.load(path, map_location="cpu", weights_only=True)
     sd = ck["state_dict0"] if "state_dict0" in ck else ck
     return {k: v.detach().cpu().numpy() for k, v in sd.items()}
+
+
+# ----------------------------------------------------------------------------------------- transform codec point
+# rate="transform" (transform_state_dict): not a trained model either, but weights that make the network a working
+# codec, so that its reconstruction quality means something on structured frames (smooth_frame).  The encoder is an
+# orthonormal 8x8 block DCT per colour (prtr_forward1) passed through the GDN chain at unit gain (beta 1, gamma 0)
+# and the identity 1x1 layers, of which the M lowest-frequency coefficients (M/3 per colour) are divided by a
+# frequency-weighted step (prtr_forward3.5); the decoder multiplies them back (prtr_inverse1) and applies the inverse
+# DCT (prtr_inverse3.5).  No neighbour prediction (the masked 3x3 taps are zero), means 0, and the context net's
+# scales are the coefficients' measured spread on synthetic frames.  Every value still flows through the same
+# closed loop, GEMMs, quantiser, entropy coder and clamp as with any other weights.
+TRANSFORM_STEP = 0.2
+
+
+def _block_dct(B: int) -> np.ndarray:
+    """[3B^2, 3B^2] orthonormal: row k = c B^2 + u B + v (colour c, frequency (u, v)), column = the block channel
+    (py B + px) 3 + c of lbic.layout."""
+    n = np.arange(B)
+    d = np.sqrt(np.where(n[:, None] == 0, 1.0 / B, 2.0 / B)) * np.cos((2 * n[None, :] + 1) * n[:, None] * np.pi / (2 * B))
+    T = np.zeros((3 * B * B, 3 * B * B))
+    for c in range(3):
+        basis = np.einsum("up,vq->uvpq", d, d).reshape(B * B, B * B)      # [(u, v), (py, px)]
+        T[c * B * B:(c + 1) * B * B, c::3] = basis
+    return T
+
+
+def smooth_frame(seed: int, H: int, W: int) -> np.ndarray:
+    """A structured synthetic frame, uint8 [3, H, W]: low-frequency cosine fields per colour, soft-edged rectangles
+    and a little noise (seeded; a stand-in for natural images, which are not available offline)."""
+    rng = np.random.default_rng(seed)
+    s = float(max(H, W))
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    img = np.empty((3, H, W))
+    for c in range(3):
+        acc = np.full((H, W), rng.uniform(0.3, 0.7))
+        for _ in range(6):
+            fx, fy = rng.uniform(0.5, 6.0, 2)
+            acc += rng.uniform(0.03, 0.12) * np.cos(2 * np.pi * (fx * xx + fy * yy) / s + rng.uniform(0, 2 * np.pi))
+        img[c] = acc
+    for _ in range(5):
+        x0, y0 = rng.integers(0, max(W - 64, 1)), rng.integers(0, max(H - 64, 1))
+        w, h = rng.integers(32, 192, 2)
+        m = (1 / (1 + np.exp(-np.minimum(xx - x0, x0 + w - xx) / 3.0))) * (1 / (1 + np.exp(-np.minimum(yy - y0, y0 + h - yy) / 3.0)))
+        col = rng.uniform(0, 1, 3)
+        img = img * (1 - m) + col[:, None, None] * m
+    img = np.clip(img + rng.normal(0, 0.01, img.shape), 0, 1)
+    return np.round(img * 255).astype(np.uint8)
+
+
+def transform_state_dict(arch: Arch, step: float = TRANSFORM_STEP, seed: int = 7) -> Dict[str, np.ndarray]:
+    B, cx, M = arch.B, arch.cx, arch.M
+    if M % 3 or M // 3 > B * B or min(arch.N, arch.n7, arch.n6) < cx:
+        raise ValueError("transform weights need M divisible by 3, M/3 <= B^2 and N, 7N/8, 6N/8 >= 3B^2")
+    T = _block_dct(B)
+    order = sorted((u + v, u, v) for u in range(B) for v in range(B))[: M // 3]
+    keep = np.array([c * B * B + u * B + v for c in range(3) for (_, u, v) in order])
+    delta = step * np.array([1.0 + 0.5 * (u + v) for c in range(3) for (_, u, v) in order])
+    # the coefficients' spread on synthetic frames -> the context net's (constant) scales
+    from .layout import image_to_blocks
+    xb = image_to_blocks(smooth_frame(seed, 256, 256).astype(np.float32) / 255.0 - 0.5, B).reshape(-1, cx)
+    q = np.rint((xb.astype(np.float64) @ T.T)[:, keep] / delta)
+    sigma = np.maximum(q.std(axis=0), 0.11)
+    out: Dict[str, np.ndarray] = {}
+    eye = np.arange(cx)
+    for name, shape in arch.param_shapes():
+        mod, leaf = name.rsplit(".", 1)
+        if leaf == "weight":
+            w = np.zeros(shape, np.float32)
+            if mod == "prtr_forward1":
+                w[:cx, :, 0, 0] = T
+            elif mod in ("prtr_forward3.1", "prtr_forward3.3", "prtr_inverse3.1", "prtr_inverse3.3"):
+                w[eye, eye, 0, 0] = 1.0
+            elif mod == "prtr_forward3.5":
+                w[np.arange(M), keep, 0, 0] = 1.0 / delta
+            elif mod == "prtr_inverse1":
+                w[keep, np.arange(M), 0, 0] = delta
+            elif mod == "prtr_inverse3.5":
+                w[:, :cx, 0, 0] = T.T
+            out[name] = w
+        elif leaf == "bias":
+            b = np.zeros(shape, np.float32)
+            if mod == "get_meanscale.6":
+                b[:M] = sigma
+            out[name] = b
+        elif leaf == "beta":      # beta_eff = 1 through the reparam (utils/parametrizers.py:42-47)
+            out[name] = np.full(shape, np.sqrt(1.0 + PEDESTAL), np.float32)
+        elif leaf == "gamma":     # gamma_eff = 0
+            out[name] = np.full(shape, np.sqrt(PEDESTAL), np.float32)
+        else:  # pragma: no cover
+            raise KeyError(name)
+    return out

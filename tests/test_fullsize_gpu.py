@@ -192,3 +192,23 @@ def test_team_full_size_roundtrip(name):
     mode = hs[0].team_stats()["mode"]
     print(f"{name} {T} x {n} x {H}x{W}: {bps:.3f} bits per symbol, {mode}")
     assert mode == ("team_sparse" if bps < 1.0 else "team_dense")
+
+
+def test_transform_point_through_library():
+    """The transform-codec weights (bench.py's quality.transform_point) through the HIP library on 768x768 structured
+    frames: decode(encode) bit-exact, and a real operating point (> 30 dB below 0.5 bpp)."""
+    from lbic.arch import Arch
+    from lbic.layout import image_to_blocks
+    from lbic.weights import smooth_frame, transform_state_dict
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    m = _model(arch, transform_state_dict(arch))
+    xb = torch.from_numpy(np.stack([image_to_blocks(smooth_frame(100 + i, 768, 768).astype(np.float32) / 255 - 0.5, 8)
+                                    for i in range(2)])).cuda()
+    r = m.compress_batch(xb)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    z = m.decompress_batch(st, 96, 96)
+    assert torch.equal(z, r["zhat"])
+    psnr = float((-10 * torch.log10(((z - xb) ** 2).double().mean(dim=(1, 2, 3)))).mean())
+    bpp = float(np.mean([len(s) * 8 / 768 ** 2 for s in st]))
+    print(f"transform point: {bpp:.4f} bpp, {psnr:.2f} dB")
+    assert psnr > 30 and bpp < 0.5, (psnr, bpp)

@@ -85,3 +85,24 @@ def test_band_rows_cover_the_frame():
     assert wavefront_steps(96, 96) == 286
     with pytest.raises(ValueError):
         band_rows(3, 4)
+
+
+def test_transform_weights_are_a_codec():
+    """lbic.weights.transform_state_dict: the block DCT is orthonormal in lbic.layout's channel order, and the CPU
+    oracle's closed loop (compress -> rANS bytes) on a structured synthetic frame reconstructs it at a real operating
+    point (tens of dB at well under 1 bpp)."""
+    from lbic.arch import Arch
+    from lbic.layout import image_to_blocks
+    from lbic.weights import _block_dct, smooth_frame, transform_state_dict
+    from oracle import oracle as O
+    T = _block_dct(8)
+    assert np.abs(T @ T.T - np.eye(192)).max() < 1e-12
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    sd = transform_state_dict(arch)
+    xb = image_to_blocks(smooth_frame(3, 64, 64).astype(np.float32) / 255 - 0.5, 8)
+    r = O.OracleCodec(arch, sd).compress(xb)
+    psnr = -10 * np.log10(np.mean((r["zhat"] - xb) ** 2))
+    bpp = len(r["bytes"]) * 8 / (64 * 64)
+    assert psnr > 28 and bpp < 1.5, (psnr, bpp)
+    with pytest.raises(ValueError):
+        transform_state_dict(Arch(4, (3, 3, 1, 1), 512, 96))    # 96 coefficients > 3 * 4^2
