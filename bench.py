@@ -85,8 +85,6 @@ def parse_args(argv=None):
                     help="headline schedule: one encoder handle compresses the batches while groups of TEAM encoded "
                          "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
                          "workgroups per 32-frame batch); 0 = the --workers / --depth schedules")
-    ap.add_argument("--fill-encoders", type=int, default=1, choices=(1, 2),
-                    help="team schedule: encoder handles compressing the first group's batches (the pipeline fill)")
     ap.add_argument("--team-groups", default="last-full", choices=("last-full", "first-full"),
                     help="when --steps is not a multiple of --team: the partial group is the first launch (last-full) "
                          "or the last one (first-full)")
@@ -397,22 +395,13 @@ def main():
 
             dth = threading.Thread(target=team_decoder)
             dth.start()
-            # the first group's batches (the fill: no decode can run beside them yet) are compressed in pairs, the
-            # second of each pair by another handle on its own stream (--fill-encoders 2)
-            nfill = sizes[0] if args.fill_encoders > 1 and len(sizes) > 1 else 0
-            with ThreadPoolExecutor(max_workers=4) as ex, ThreadPoolExecutor(max_workers=1) as fx:
-                k = 0
-                while k < steps:
-                    pair = k + 1 < nfill
-                    if pair:
-                        f2 = fx.submit(compress_side, ph, frames_of(base + k + 1), dec_models[-1], s_decs[-1])
-                    batch = [compress_side(ph, frames_of(base + k))] + ([f2.result()] if pair else [])
-                    for r_ in batch:
-                        f_ = ex.submit(entropy_side, r_, fmt, ph)
-                        # only the last batch keeps its record (zhat, symbols) for the quality check
-                        dq.put((base + k, r_ if k == steps - 1 else None, f_))
-                        k += 1
-                    del batch
+            with ThreadPoolExecutor(max_workers=4) as ex:
+                for k in range(steps):
+                    r_ = compress_side(ph, frames_of(base + k))
+                    f_ = ex.submit(entropy_side, r_, fmt, ph)
+                    # only the last batch keeps its record (zhat, symbols) for the quality check
+                    dq.put((base + k, r_ if k == steps - 1 else None, f_))
+                    del r_
                 dq.put(None)
                 dth.join()
             if errs:
