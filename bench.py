@@ -54,6 +54,7 @@ METRIC = "Mpixels/s encode+decode, B8_lowrate N768M96, 768×768; bpp/PSNR vs ref
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA (dense) peak
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E peak (spec)
 
+CONFIG_LAMBDA = {"B8_lowrate": 117.045, "B8_highrate": 11704.5, "B4_highrate": 11704.5, "B16_lowrate": 117.045}
 CONFIGS = {   # name -> (B, KS, N, M)
     "B8_lowrate": (8, (3, 1, 1, 1), 768, 96),
     "B8_highrate": (8, (3, 3, 1, 1), 1152, 128),
@@ -77,7 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--size", type=int, default=768, help="frame width (and height unless --height)")
     ap.add_argument("--height", type=int, default=0, help="frame height (default: --size)")
     ap.add_argument("--config", default="B8_lowrate", choices=sorted(CONFIGS))
-    ap.add_argument("--rate", default="low", choices=("low", "high"), help="synthetic weight operating point")
+    ap.add_argument("--rate", default="", choices=("", "low", "mid", "high"),
+                    help="synthetic weight operating point (default: the config's, lbic.weights.rate_for_lambda: 'low' "
+                         "for the lambda-117 configs, 'mid' = ~1.6 bpp for the high-rate ones; 'high' = the 12-47 bpp set)")
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
     ap.add_argument("--share-weights", type=int, default=1,
                     help="1: decoder handles share the encoder handle's device weights (lbc_create_sibling)")
@@ -109,6 +112,13 @@ def parse_args(argv=None):
                          "the same-command rocprof summary holds only the headline's kernel shapes)")
     ap.add_argument("--substream-steps", type=int, default=0, help="batches in the opt-in sub-stream format (0 = skip)")
     ap.add_argument("--encode-only", type=int, default=0, help="profiling aid: this many encoder passes, no JSON")
+    ap.add_argument("--team-xs", type=int, default=-1, choices=(-1, 0, 1),
+                    help="team decoder geometry: 1 column-split teams (each team spans the 8 XCD slots, each slot a fixed "
+                         "eighth of every GEMM's columns: the decoder weights stay L2-resident), 0 one XCD slot per team, "
+                         "-1 the library default (LBIC_TEAM_XS)")
+    ap.add_argument("--per-image", type=int, default=1,
+                    help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
+                         "compress() then decompress() of ONE frame, batch 1), median of 3")
     return ap.parse_args(argv)
 
 
@@ -194,11 +204,21 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     dist = world > 1
+    if args.team_xs >= 0:
+        os.environ["LBIC_TEAM_XS"] = str(args.team_xs)
+    # test hooks (tests/test_bench_dist_gpu.py runs the N-rank path on a one-GPU box): every rank on one device, and the
+    # gloo backend (RCCL refuses two ranks on one GPU).  The driver's runs set neither: one GPU per rank, RCCL.
+    local = int(os.environ.get("LBIC_BENCH_DEVICE", local))
+    backend = os.environ.get("LBIC_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = torch.device("cpu") if backend == "gloo" else dev     # where collective operands live
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group(backend, device_id=dev)
 
     import types
     from lbic.arch import Arch
@@ -208,6 +228,9 @@ def main():
     from lbic.weights import synth_state_dict
 
     B, KS, N, M = CONFIGS[args.config]
+    if not args.rate:
+        from lbic.weights import rate_for_lambda
+        args.rate = rate_for_lambda(CONFIG_LAMBDA[args.config])
     arch = Arch(B, KS, N, M)
     W = args.size
     H = args.height or args.size
@@ -255,7 +278,7 @@ def main():
 
     def max_over_ranks(v):
         if dist:
-            t = torch.tensor([v], dtype=torch.float64, device=dev)
+            t = torch.tensor([v], dtype=torch.float64, device=coll_dev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             v = float(t.item())
         return v
@@ -307,7 +330,7 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[])
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, column_split=[])
 
     def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
@@ -344,7 +367,9 @@ def main():
             dq = queue.Queue(maxsize=2 * team)
             if prof:
                 for kk in team_acc:
-                    team_acc[kk] = [] if kk == "plain" else 0
+                    team_acc[kk] = [] if kk in ("plain", "column_split") else 0
+                team_acc["hw"] = Hb * Wb
+                to0 = dec_models[0].team_stats()["timeout_fallbacks"]
             errs = []
 
             # group sizes: with --team-groups last-full (default) a partial group comes FIRST, so the launch that
@@ -383,6 +408,8 @@ def main():
                                 team_acc["flops"] += st_["flops"]
                                 team_acc["steps"] += len(pend) * Hb * Wb
                                 team_acc["plain"].append(st_["plain"])
+                                team_acc["column_split"].append(st_["column_split"])
+                                team_acc["timeouts"] = st_["timeout_fallbacks"] - to0
                             for (k_, r_, _), st_, z_ in zip(pend, sts, zs):
                                 finish(k_, r_, st_, z_)
                             pend = []
@@ -495,14 +522,15 @@ def main():
             for th in ths:
                 th.join()
         barrier()
-        dt = max_over_ranks(time.perf_counter() - t0)
+        local_dt = time.perf_counter() - t0
+        dt = max_over_ranks(local_dt)
         if prof:
             enc_acc["on"] = False
             torch.cuda._sleep(1000)
             torch.cuda.synchronize(dev)
         ks = collect_stats() if prof else None
         if label:
-            log(f"[rank {rank}] {label}: {steps} batches in {dt:.2f} s")
+            log(f"[rank {rank}] {label}: {steps} batches in {dt:.2f} s (this rank {local_dt:.4f} s)")
         if done["count"] != steps:
             raise RuntimeError(f"{label}: {done['count']} of {steps} batches decoded")
         return dt, ph, done["last"][1:], ks
@@ -574,15 +602,17 @@ def main():
     sse = ((z - xq) ** 2).double().sum(dim=(1, 2, 3))
     rec = torch.stack([torch.tensor([float(len(s)) for s in streams], dtype=torch.float64, device=dev), sse,
                        torch.full((n,), float(H * W * 3), dtype=torch.float64, device=dev)], dim=1)
-    rec, bit_exact = gather_records(rec, bit_exact, dist)
+    rec, bit_exact = gather_records(rec.to(coll_dev), bit_exact, dist)
     rec = rec.cpu().numpy()
     bpp = float(np.mean(rec[:, 0] * 8.0 / (H * W)))
     psnr = float(np.mean(-10 * np.log10(rec[:, 1] / rec[:, 2])))
-    vs_ref = tq = None
+    vs_ref = tq = per_img = None
     if rank == 0:
         vs_ref = compare_full_frame_fixture(enc_model, args, arch, dev)
         if args.side_steps > 0:
             tq = transform_quality(arch, cfg, dev, H, W)
+        if args.per_image:
+            per_img = per_image_timing(enc_model, dec_models, arch, H, W, dev)
 
     if rank != 0:
         if dist:
@@ -632,7 +662,9 @@ def main():
                      "included"},
         "roofline": roof, "cpu_baseline": cpu,
         "quality": {"rate_point": args.rate, "bpp": round(bpp, 5), "psnr_db": round(psnr, 3),
-                    "enc_dec_bit_exact": bit_exact, "vs_ref": vs_ref, "transform_point": tq},
+                    "enc_dec_bit_exact": bit_exact, "images_gathered": int(rec.shape[0]), "vs_ref": vs_ref,
+                    "transform_point": tq},
+        "per_image": per_img,
         "phases_ms_per_step": {k: round(v / args.steps * 1e3, 2) for k, v in phase.items()},
         "step_algorithmic_tflop": round(step_flops / 1e12, 3),
         "step_mfma_frac": round(step_flops / (dt / args.steps) / (PEAK_FP32_TFLOPS * 1e12), 5),
@@ -695,7 +727,12 @@ def roofline(kstats, dt, team=None, enc=None):
         kernels["k_dec_team"] = dict(launches_sampled=team["launches"], launches_total=team["launches"],
                                      avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
                                      est_share_of_step=round(team["ms"] / 1e3 / dt, 4),
-                                     plain_handoffs=team["plain"], timing="HIP events around each launch")
+                                     plain_handoffs=team["plain"], column_split=team["column_split"],
+                                     barrier_timeout_fallbacks=team["timeouts"],
+                                     batches_per_launch=round(team["steps"] / team["launches"] / team["hw"], 3),
+                                     batch_decode_latency_ms=round(per, 3),
+                                     launch_ms_per_batch=round(team["ms"] * team["hw"] / team["steps"], 3),
+                                     timing="HIP events around each launch")
         fam["k_dec_team"] = (team["flops"] / team["launches"], team["bytes"] / team["launches"])
     if not kernels:
         return None, {}
@@ -726,6 +763,46 @@ def roofline(kstats, dt, team=None, enc=None):
                 frac_of_span=round((fl / (kernels[dom]["avg_span_us"] * 1e-6) / 1e12 / peak) if bound == "mfma" else
                                    (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5))
     return roof, kernels
+
+
+def per_image_timing(enc_model, dec_models, arch, H, W, dev, reps=3):
+    """The reference's per-image timed region (eval_model, agents/blkbsdimgcomp_agent.py:591-599): compress() of ONE
+    frame (batch 1: GPU wavefront + host rANS) and decompress() of its bitstream, each bracketed by
+    torch.cuda.synchronize() and timed on the host clock as the reference does, through the reference interface
+    (lbic.model: compress / decompress -> lbc_encode + lbc_rans_encode / lbc_decode).  Beside it, the same bitstream
+    through a team launch of one batch (decompress_teams, T = 1).  Median of `reps` (after one untimed pass)."""
+    import numpy as np
+    import torch
+    from lbic.layout import image_to_blocks
+    from lbic.model import decompress_teams
+    img = np.random.default_rng(12345).integers(0, 256, (3, H, W), dtype=np.uint8).astype(np.float32) / 255.0 - 0.5
+    xb = torch.from_numpy(image_to_blocks(img, arch.B)).to(dev)
+    x = xb.permute(2, 0, 1)[None].contiguous()            # [1, 3B^2, Hb, Wb], the reference's layout
+    lru = [arch.lru] * 3
+    enc, dec, team = [], [], []
+    for k in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.time()
+        bs, zhat = enc_model.compress(x, lru, arch.M)
+        torch.cuda.synchronize(dev)
+        t1 = time.time()
+        z = dec_models[0].decompress(bs, lru, x.shape, arch.M, dev)
+        torch.cuda.synchronize(dev)
+        t2 = time.time()
+        zt = decompress_teams(dec_models[:1], [[bs]], H // arch.B, W // arch.B)[0]
+        torch.cuda.synchronize(dev)
+        t3 = time.time()
+        if k:
+            enc.append(t1 - t0)
+            dec.append(t2 - t1)
+            team.append(t3 - t2)
+        exact = bool(torch.equal(z, zhat)) and bool(torch.equal(zt[0], zhat[0].permute(1, 2, 0)))
+    med = lambda v: round(float(np.median(v)) * 1e3, 2)
+    return dict(frame=[H, W], bpp=round(len(bs) * 8.0 / (H * W), 5), enc_ms=med(enc), dec_ms=med(dec),
+                dec_team_ms=med(team), enc_dec_bit_exact=exact,
+                note="eval_model's per-image Enc/DecTime (batch 1, host clock around synchronize): compress() = "
+                     "lbc_encode + host rANS, decompress() = lbc_decode (raster graph decoder); dec_team_ms: the same "
+                     "stream through one k_dec_team launch (decompress_teams, one batch)")
 
 
 def transform_quality(arch, cfg, dev, H, W, n=4):

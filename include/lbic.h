@@ -161,6 +161,12 @@ int lbc_team_stats(const lbc_model *m, double *launch_ms, double *bytes, double 
 /* how the last lbc_decode_team call led by m decoded: 0 lbc_decode per batch (fallback), 1 one team launch with the
  * sparse rANS variant, 2 one team launch with the dense variant (tables in LDS). */
 int lbc_team_mode(const lbc_model *m, int *mode);
+/* counters of the lbc_decode_team calls led by m: launches rerun with write-through hand-offs after the placement
+ * census found a team spread over XCDs; launches in which a workgroup timed out at a team barrier (the grid was not
+ * co-resident in time, e.g. CUs held by another process) and whose batches were then decoded by lbc_decode one after
+ * another (same results); and whether the last team launch ran column-split (1: every team spans all 8 XCD slots, each
+ * slot computing a fixed 1/8 of every GEMM's columns, LBIC_TEAM_XS=1) or one XCD slot per team (0). */
+int lbc_team_events(const lbc_model *m, int *sc1_reruns, int *timeouts, int *column_split);
 
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder

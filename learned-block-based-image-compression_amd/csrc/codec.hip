@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -138,9 +139,15 @@ struct Work {
 };
 
 // The packed device weights of one finalized state dict: shared (read-only) by every handle made from it with
-// lbc_create_sibling, so several handles decoding side by side keep one copy in the Infinity Cache
+// lbc_create_sibling, so several handles decoding side by side keep one copy in the Infinity Cache.  gen: a
+// process-unique id of this packed set (recorded programs key on it: a new set may reuse freed addresses)
 struct Net {
     Layer ctx0, ctx1, ctx2, ctx3, enc0, g0, e1, g1, e2, g2, e3, dec0, ig0, d1, ig1, d2, ig2, d3;
+    long long gen = next_gen();
+    static long long next_gen() {
+        static std::atomic<long long> g{0};
+        return ++g;
+    }
 };
 
 static const int TAPS_A[4][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}};       // masked_conv2d.py:9-17 'A'
@@ -205,6 +212,8 @@ struct lbc_model {
     TeamArgs team_args{};
     std::vector<unsigned long long> team_ts_host;
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
+    int team_timeouts = 0;    // team launches that timed out at a barrier and were decoded through lbc_decode instead
+    int team_xs_last = 0;     // the last team launch ran column-split (TeamArgs::xs)
     int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
@@ -880,9 +889,34 @@ int lbc_set_tensor(lbc_model* m, const char* name, const float* host, const int6
 int lbc_finalize(lbc_model* m) {
     if (!m) return set_error(LBC_E_ARG, "null model");
     HIPCHK(hipSetDevice(m->cfg.device));
-    m->finalized = false;
-    m->net = std::make_shared<Net>();     // a new packed set: siblings made earlier keep theirs
-    // the captured graphs hold the old weight pointers
+    // pack into a new set and install it only when every layer packed: a failing call (or one on a sibling, which
+    // holds no host tensors) leaves the handle's working weights, graphs and finalized state untouched
+    auto net = std::make_shared<Net>();   // a new packed set: siblings made earlier keep theirs
+    const int Cx = m->Cx, N = m->N, M = m->M;
+    static const int one[1][2] = {{0, 0}};
+    int rc;
+    // context net: layer 0 = 4 masked taps; layer 1 = 1x1, or 3x3 'B' over the 5 layer-0 positions
+    if ((rc = pack_conv(m, net->ctx0, "get_meanscale.0", Cx, m->C1, 4, TAPS_A))) return rc;
+    if (m->P == 5) rc = pack_conv(m, net->ctx1, "get_meanscale.2", m->C1, m->C2, 5, TAPS_B);
+    else rc = pack_conv(m, net->ctx1, "get_meanscale.2", m->C1, m->C2, 1, one);
+    if (rc) return rc;
+    if ((rc = pack_conv(m, net->ctx2, "get_meanscale.4", m->C2, m->C3, 1, one))) return rc;
+    if ((rc = pack_conv(m, net->ctx3, "get_meanscale.6", m->C3, m->C4, 1, one))) return rc;
+    if ((rc = pack_first(m, net->enc0, "prtr_forward2", "prtr_forward1", Cx))) return rc;
+    if ((rc = pack_gdn(m, net->g0, "prtr_forward3.0", N))) return rc;
+    if ((rc = pack_conv(m, net->e1, "prtr_forward3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, net->g1, "prtr_forward3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, net->e2, "prtr_forward3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, net->g2, "prtr_forward3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, net->e3, "prtr_forward3.5", m->N6, M, 1, one))) return rc;
+    if ((rc = pack_first(m, net->dec0, "prtr_inverse2", "prtr_inverse1", M))) return rc;
+    if ((rc = pack_gdn(m, net->ig0, "prtr_inverse3.0", N))) return rc;
+    if ((rc = pack_conv(m, net->d1, "prtr_inverse3.1", N, m->N7, 1, one))) return rc;
+    if ((rc = pack_gdn(m, net->ig1, "prtr_inverse3.2", m->N7))) return rc;
+    if ((rc = pack_conv(m, net->d2, "prtr_inverse3.3", m->N7, m->N6, 1, one))) return rc;
+    if ((rc = pack_gdn(m, net->ig2, "prtr_inverse3.4", m->N6))) return rc;
+    if ((rc = pack_conv(m, net->d3, "prtr_inverse3.5", m->N6, Cx, 1, one))) return rc;
+    // the captured graphs and the recorded team program hold the old weight pointers
     if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
     if (m->wf_exec) { (void)hipGraphExecDestroy(m->wf_exec); m->wf_exec = nullptr; }
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
@@ -890,30 +924,8 @@ int lbc_finalize(lbc_model* m) {
     for (auto& kv : m->band_exec) (void)hipGraphExecDestroy(kv.second);
     m->band_exec.clear();
     m->band_key.clear();
-    const int Cx = m->Cx, N = m->N, M = m->M;
-    static const int one[1][2] = {{0, 0}};
-    int rc;
-    // context net: layer 0 = 4 masked taps; layer 1 = 1x1, or 3x3 'B' over the 5 layer-0 positions
-    if ((rc = pack_conv(m, m->net->ctx0, "get_meanscale.0", Cx, m->C1, 4, TAPS_A))) return rc;
-    if (m->P == 5) rc = pack_conv(m, m->net->ctx1, "get_meanscale.2", m->C1, m->C2, 5, TAPS_B);
-    else rc = pack_conv(m, m->net->ctx1, "get_meanscale.2", m->C1, m->C2, 1, one);
-    if (rc) return rc;
-    if ((rc = pack_conv(m, m->net->ctx2, "get_meanscale.4", m->C2, m->C3, 1, one))) return rc;
-    if ((rc = pack_conv(m, m->net->ctx3, "get_meanscale.6", m->C3, m->C4, 1, one))) return rc;
-    if ((rc = pack_first(m, m->net->enc0, "prtr_forward2", "prtr_forward1", Cx))) return rc;
-    if ((rc = pack_gdn(m, m->net->g0, "prtr_forward3.0", N))) return rc;
-    if ((rc = pack_conv(m, m->net->e1, "prtr_forward3.1", N, m->N7, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->net->g1, "prtr_forward3.2", m->N7))) return rc;
-    if ((rc = pack_conv(m, m->net->e2, "prtr_forward3.3", m->N7, m->N6, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->net->g2, "prtr_forward3.4", m->N6))) return rc;
-    if ((rc = pack_conv(m, m->net->e3, "prtr_forward3.5", m->N6, M, 1, one))) return rc;
-    if ((rc = pack_first(m, m->net->dec0, "prtr_inverse2", "prtr_inverse1", M))) return rc;
-    if ((rc = pack_gdn(m, m->net->ig0, "prtr_inverse3.0", N))) return rc;
-    if ((rc = pack_conv(m, m->net->d1, "prtr_inverse3.1", N, m->N7, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->net->ig1, "prtr_inverse3.2", m->N7))) return rc;
-    if ((rc = pack_conv(m, m->net->d2, "prtr_inverse3.3", m->N7, m->N6, 1, one))) return rc;
-    if ((rc = pack_gdn(m, m->net->ig2, "prtr_inverse3.4", m->N6))) return rc;
-    if ((rc = pack_conv(m, m->net->d3, "prtr_inverse3.5", m->N6, Cx, 1, one))) return rc;
+    m->team_key.clear();
+    m->net = std::move(net);
     m->finalized = true;
     return LBC_OK;
 }
@@ -1348,6 +1360,136 @@ static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* stre
     return LBC_OK;
 }
 
+// The team program (held by ms[0]): every team's raster step recorded from the same run_ctx / run_dec calls that build
+// the graph decoder, for the geometry (S, spread, xs, W); rebuilt when the geometry, any team's buffers or any team's
+// weight set (Net::gen) changed.  Sets ms[0]->team_args (without the per-launch fields) and the step's algorithmic work.
+static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, int S, int spread, int xs, int W,
+                       int sparse) {
+    lbc_model* m0 = ms[0];
+    int rc;
+    std::vector<long long> key = {T, S, spread, xs, W, n_img, Hb, Wb, sparse};
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        for (long long x : {(long long)m->words.p, (long long)m->zpad.p, (long long)m->lane[0].ctx0.p,
+                            (long long)m->lane[0].d0.p, (long long)m->table_dev.p, (long long)m->tmeta_dev.p,
+                            (long long)m->st_x.p, (long long)m->l0.p, m->net->gen})
+            key.push_back(x);
+    }
+    if (key == m0->team_key) return LBC_OK;
+    std::vector<GemmArgs> gem;
+    std::vector<RansArgs> rans;
+    std::vector<int> ops;
+    int NG = -1;
+    for (int t = 0; t < T; ++t) {
+        lbc_model* m = ms[t];
+        Work& w = m->lane[0];
+        for (int c = 0; c < 3; ++c) {
+            const int hc = c == 0 ? 0 : c == 1 ? std::min(1, Wb - 1) : Wb - 1;
+            Recorder rec;
+            GemmArgs g = base_args(m, m->blocks_dec.as<int4>(), n_img, nullptr, n_img, Hb, Wb);
+            g.ctr = m->ctr.as<int>();
+            g.ctr_stride = Wb * n_img;
+            g.raster = 1;
+            g.raster_img0 = 0;
+            g.raster_h = hc;
+            g_rec = &rec;
+            int crc = run_ctx(m, w, g, true, nullptr);
+            rec.ops.push_back(-1);
+            if (!crc) crc = run_dec(m, w, g, nullptr);
+            g_rec = nullptr;
+            if (crc) return crc;
+            if (NG < 0) {
+                NG = (int)rec.gemms.size();
+                ops = rec.ops;
+            }
+            if ((int)rec.gemms.size() != NG || rec.ops != ops || (int)ops.size() > TEAM_MAXOPS)
+                return set_error(LBC_E_STATE, "team decoder: raster steps differ in shape");
+            gem.insert(gem.end(), rec.gemms.begin(), rec.gemms.end());
+        }
+        RansArgs r = rans_args(m);
+        r.idx = w.idx.as<int32_t>();
+        r.ksi = w.ksi.as<float>();
+        r.yq = w.yq.as<float>();
+        r.rows = n_img;
+        r.sparse = sparse;
+        rans.push_back(r);
+    }
+    const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
+    if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
+    HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
+    if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned)))) return rc;
+    if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
+    TeamArgs& a = m0->team_args;
+    a = TeamArgs{};
+    a.gemm = m0->team_prog.as<GemmArgs>();
+    a.rans = reinterpret_cast<const RansArgs*>(static_cast<char*>(m0->team_prog.p) + gb);
+    for (size_t i = 0; i < ops.size(); ++i) a.opk[i] = ops[i];
+    a.nops = (int)ops.size();
+    a.NG = NG;
+    a.T = T;
+    a.S = S;
+    a.spread = spread;
+    a.xs = xs;
+    a.W = W;
+    a.Hb = Hb;
+    a.Wb = Wb;
+    a.sync = m0->team_sync.as<unsigned>();
+    // a GEMM's tile share: S workgroups over all column tiles, or (xs) W workgroups over the widest slot's columns
+    auto share = [&](const GemmArgs& d, int& gS, int& ntn) {
+        const int NT = (d.N + 15) >> 4;
+        gS = xs ? W : S;
+        ntn = xs ? (NT + TEAM_MAX - 1) / TEAM_MAX : NT;
+    };
+    // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
+    a.ni_max = 2;
+    a.tab16 = rans[0].total16;
+    for (const GemmArgs& d : gem) {
+        int gS, ntn;
+        share(d, gS, ntn);
+        const int items = ((d.M + 15) >> 4) * ntn;
+        if (team_fast_path(d, gS, ntn)) a.ni_max = std::max(a.ni_max, (items + gS - 1) / gS);
+    }
+    // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
+    // before it run beside the rANS decode when every workgroup takes the fast path for it
+    a.split_op = -1;
+    a.split_wy = 0;
+    for (int i = 0; i + 1 < (int)ops.size(); ++i) {
+        if (ops[i] != -1 || ops[i + 1] < 0 || getenv("LBIC_TEAM_NOSPLIT")) continue;
+        bool fast = true;
+        for (int t = 0; t < T; ++t)
+            for (int c = 0; c < 3; ++c) {
+                const GemmArgs& d = gem[((size_t)t * 3 + c) * NG + ops[i + 1]];
+                int gS, ntn;
+                share(d, gS, ntn);
+                fast = fast && team_fast_path(d, gS, ntn);
+            }
+        const GemmArgs& d = gem[ops[i + 1]];
+        const Seg& last = d.seg[d.nseg - 1];
+        if (last.kind != SEG_DENSE || last.base != ms[0]->lane[0].yq.as<float>() || !fast) continue;
+        const int nkb = d.K >> 4, kby = last.k0 >> 4;
+        int wy = 0;
+        while (wy < KSPLIT && (wy + 1) * nkb / KSPLIT <= kby) ++wy;
+        if (wy >= 1 && wy <= KSPLIT - 1) {
+            a.split_op = i + 1;
+            a.split_wy = wy;
+        }
+    }
+    // algorithmic work of one raster step (the graph decoder's accounting, gemm(): weights + A rows + outputs [+ the
+    // GDN input] once per GEMM; rANS: indexes and means in, y_qnt out, the step's stream words)
+    double sb = 0, sf = 0;
+    for (int gi = 0; gi < NG; ++gi) {
+        const GemmArgs& d = gem[(size_t)1 * NG + gi];     // team 0, inner column class
+        sb += 4.0 * ((double)d.K * d.N + (double)d.M * d.K + (double)d.M * d.N * (d.square_a ? 2 : 1));
+        sf += 2.0 * d.M * d.K * d.N;
+    }
+    sb += 12.0 * n_img * m0->M;
+    m0->team_step_bytes = sb;
+    m0->team_step_flops = sf;
+    m0->team_key = key;
+    return LBC_OK;
+}
+
 int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* streams, const size_t* lens, int n_img,
                     int Hb, int Wb, float* const* zhat_devs, void* stream) {
     if (!ms || !streams || !lens || !zhat_devs) return set_error(LBC_E_ARG, "null argument");
@@ -1378,18 +1520,6 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     int dev = m0->cfg.device, cus = 0;
     HIPCHK(hipSetDevice(dev));
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int per_cu = team_blocks_per_cu();
-    // grid 8 x S: one XCD slot per team (k_dec_team); S = one (or, LBC_OPT_TEAM_WG_PER_CU, two) workgroups per CU
-    // of an XCD -- the whole grid must be resident (team barriers), so never more than the occupancy allows
-    const int wpc = std::min(m0->team_wpc, per_cu);
-    int S = std::min(32, cus / TEAM_MAX) * std::max(wpc, 1);
-    if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
-    // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches alone:
-    // 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD per team
-    const char* spe = getenv("LBIC_TEAM_SPREAD");
-    const int spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
-    S *= spread;
-    if (S < 1 || per_cu < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     for (int t = 0; t < T; ++t) {
         lbc_model* m = ms[t];
         if ((rc = prepare_device(m))) return rc;
@@ -1399,133 +1529,69 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[(size_t)t * n_img + i], lens[(size_t)t * n_img + i]);
         if ((rc = upload_streams(m, subs, s))) return rc;
     }
-    // the recorded program, rebuilt when any team's buffers or weights moved
-    std::vector<long long> key = {T, S, spread, n_img, Hb, Wb};
-    for (int t = 0; t < T; ++t) {
-        lbc_model* m = ms[t];
-        for (long long x : {(long long)m->words.p, (long long)m->zpad.p, (long long)m->lane[0].ctx0.p,
-                            (long long)m->lane[0].d0.p, (long long)m->table_dev.p, (long long)m->tmeta_dev.p,
-                            (long long)m->st_x.p, (long long)m->l0.p, (long long)m->net->ctx0.W.p,
-                            (long long)m->net->d3.W.p})
-            key.push_back(x);
+    // team geometry.  Default (xs = 0): grid 8 x S, one XCD slot per team, S = one (or, LBC_OPT_TEAM_WG_PER_CU, two)
+    // workgroups per CU of an XCD.  Column-split (xs = 1, LBIC_TEAM_XS): every team has W workgroups on each of the 8
+    // slots, W = (workgroups per slot) / T, and the slots split every GEMM's columns.  The whole grid must be resident
+    // (team barriers): the occupancy query below uses the kernel instance and the dynamic LDS of the launch, and a
+    // geometry that does not fit is shrunk (two workgroups per CU -> one) or decoded by lbc_decode per batch.
+    const char* xse = getenv("LBIC_TEAM_XS");
+    const int xs = xse ? (atoi(xse) != 0) : 0;
+    int wpc = std::max(1, m0->team_wpc);
+    int S = 0, spread = 1, W = 0;
+    TeamArgs a{};
+    for (;;) {
+        const int per_slot = std::min(32, cus / TEAM_MAX) * wpc;
+        if (xs) {
+            W = per_slot / T;
+            S = 8 * W;
+            spread = 1;
+        } else {
+            S = per_slot;
+            if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
+            // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
+            // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD
+            const char* spe = getenv("LBIC_TEAM_SPREAD");
+            spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
+            S *= spread;
+        }
+        if (S < 1 || (xs && W < 1)) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+        if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, xs, W, sparse))) return rc;
+        a = m0->team_args;
+        a.dense = sparse ? 0 : 1;   // high rates: the tables staged in every workgroup's LDS (rans_row<true>)
+        const size_t lds = team_lds_bytes(a);
+        if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+        const int nb = team_blocks_per_cu(a.dense, lds);
+        if (nb >= wpc) break;
+        if (nb < 1 || wpc == 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+        wpc = nb;
     }
-    if (key != m0->team_key) {
-        std::vector<GemmArgs> gem;
-        std::vector<RansArgs> rans;
-        std::vector<int> ops;
-        int NG = -1;
-        for (int t = 0; t < T; ++t) {
-            lbc_model* m = ms[t];
-            Work& w = m->lane[0];
-            for (int c = 0; c < 3; ++c) {
-                const int hc = c == 0 ? 0 : c == 1 ? std::min(1, Wb - 1) : Wb - 1;
-                Recorder rec;
-                GemmArgs g = base_args(m, m->blocks_dec.as<int4>(), n_img, nullptr, n_img, Hb, Wb);
-                g.ctr = m->ctr.as<int>();
-                g.ctr_stride = Wb * n_img;
-                g.raster = 1;
-                g.raster_img0 = 0;
-                g.raster_h = hc;
-                g_rec = &rec;
-                int crc = run_ctx(m, w, g, true, nullptr);
-                rec.ops.push_back(-1);
-                if (!crc) crc = run_dec(m, w, g, nullptr);
-                g_rec = nullptr;
-                if (crc) return crc;
-                if (NG < 0) {
-                    NG = (int)rec.gemms.size();
-                    ops = rec.ops;
-                }
-                if ((int)rec.gemms.size() != NG || rec.ops != ops || (int)ops.size() > TEAM_MAXOPS)
-                    return set_error(LBC_E_STATE, "team decoder: raster steps differ in shape");
-                gem.insert(gem.end(), rec.gemms.begin(), rec.gemms.end());
-            }
-            RansArgs r = rans_args(m);
-            r.idx = w.idx.as<int32_t>();
-            r.ksi = w.ksi.as<float>();
-            r.yq = w.yq.as<float>();
-            r.rows = n_img;
-            r.sparse = sparse;
-            rans.push_back(r);
-        }
-        const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
-        if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
-        HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
-        if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned)))) return rc;
-        if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
-        TeamArgs& a = m0->team_args;
-        a = TeamArgs{};
-        a.gemm = m0->team_prog.as<GemmArgs>();
-        a.rans = reinterpret_cast<const RansArgs*>(static_cast<char*>(m0->team_prog.p) + gb);
-        for (size_t i = 0; i < ops.size(); ++i) a.opk[i] = ops[i];
-        a.nops = (int)ops.size();
-        a.NG = NG;
-        a.T = T;
-        a.S = S;
-        a.spread = spread;
-        a.Hb = Hb;
-        a.Wb = Wb;
-        a.sync = m0->team_sync.as<unsigned>();
-        // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
-        a.ni_max = 2;
-        a.tab16 = rans[0].total16;
-        for (const GemmArgs& d : gem) {
-            const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
-            if (team_fast_path(d, S)) a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
-        }
-        // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices
-        // that end before it run beside the rANS decode when every workgroup takes the fast path for it
-        a.split_op = -1;
-        a.split_wy = 0;
-        for (int i = 0; i + 1 < (int)ops.size(); ++i) {
-            if (ops[i] != -1 || ops[i + 1] < 0 || getenv("LBIC_TEAM_NOSPLIT")) continue;
-            const GemmArgs& d = gem[ops[i + 1]];
-            const Seg& last = d.seg[d.nseg - 1];
-            if (last.kind != SEG_DENSE || last.base != ms[0]->lane[0].yq.as<float>() || !team_fast_path(d, S)) continue;
-            const int nkb = d.K >> 4, kby = last.k0 >> 4;
-            int wy = 0;
-            while (wy < KSPLIT && (wy + 1) * nkb / KSPLIT <= kby) ++wy;
-            if (wy >= 1 && wy <= KSPLIT - 1) {
-                a.split_op = i + 1;
-                a.split_wy = wy;
-            }
-        }
-        // algorithmic work of one raster step (the graph decoder's accounting, gemm(): weights + A rows + outputs
-        // [+ the GDN input] once per GEMM; rANS: indexes and means in, y_qnt out, the step's stream words)
-        double sb = 0, sf = 0;
-        for (int gi = 0; gi < NG; ++gi) {
-            const GemmArgs& d = gem[(size_t)1 * NG + gi];     // team 0, inner column class
-            sb += 4.0 * ((double)d.K * d.N + (double)d.M * d.K + (double)d.M * d.N * (d.square_a ? 2 : 1));
-            sf += 2.0 * d.M * d.K * d.N;
-        }
-        sb += 12.0 * n_img * m0->M;
-        m0->team_step_bytes = sb;
-        m0->team_step_flops = sf;
-        m0->team_key = key;
-    }
-    TeamArgs a = m0->team_args;
-    a.dense = sparse ? 0 : 1;   // high rates: the tables staged in every workgroup's LDS (rans_row<true>)
-    if (team_lds_bytes(a) > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
-    a.tmo = 100000000ull;                    // 1 s at one barrier: far above any operation's time
+    const char* tmoe = getenv("LBIC_TEAM_TMO");   // test hook: s_memrealtime ticks one barrier waits (default 1 s)
+    a.tmo = tmoe ? std::max(1ull, strtoull(tmoe, nullptr, 10)) : 100000000ull;
     const char* st = getenv("LBIC_TEAM_STAMPS");
     a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
     const char* pfe = getenv("LBIC_TEAM_PF");   // weight tiles of the next GEMM requested at each barrier (0..2)
-    a.pf = pfe ? std::max(0, std::min(2, atoi(pfe))) : 0;
+    a.pf = pfe && !xs ? std::max(0, std::min(2, atoi(pfe))) : 0;
     a.sv = Hb / 2;
     a.sh = Wb / 2;
-    for (int t = 0; t < T; ++t) {
-        lbc_model* m = ms[t];
-        HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
-        if (m->l0_on && (rc = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s)))
-            return rc;
-    }
-    // plain hand-off stores unless LBIC_TEAM_SC1=1; a launch that finds a team spread over XCDs stops before its
-    // first operation (failure word 2, nothing decoded yet) and is rerun with write-through hand-offs
+    auto reset = [&]() -> int {
+        for (int t = 0; t < T; ++t) {
+            lbc_model* m = ms[t];
+            HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+            int rc_;
+            if (m->l0_on &&
+                (rc_ = launch_l0_border(m->l0.as<float>(), n_img, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s)))
+                return rc_;
+        }
+        return LBC_OK;
+    };
+    // plain hand-off stores unless LBIC_TEAM_SC1=1 (or a spread / column-split geometry); a launch that finds a team
+    // spread over XCDs stops before its first operation (failure word 2, nothing decoded yet) and is rerun with
+    // write-through hand-offs
     const char* sc1e = getenv("LBIC_TEAM_SC1");
-    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 ? 0 : 1;
+    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 || a.xs ? 0 : 1;
     unsigned fail = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
+        if ((rc = reset())) return rc;
         HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));
         if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 256 * sizeof(unsigned long long), s));
         HIPCHK(hipEventRecord(m0->ev[2], s));
@@ -1537,8 +1603,18 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.plain = 0;
         m0->team_fallbacks += 1;
     }
+    if (fail) {
+        // a workgroup gave up waiting at a team barrier (the grid was not co-resident in time: another process or
+        // stream held CUs past the timeout).  Nothing is wrong with the streams: decode the batches again through
+        // lbc_decode one after another (it re-uploads the streams and resets the workspaces), and count the event.
+        m0->team_timeouts += 1;
+        if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
+            fprintf(stderr, "[lbic] team decode: barrier timeout (fail=%u), decoding through lbc_decode\n", fail);
+        return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+    }
     m0->team_plain_last = a.plain;
     m0->team_mode_last = a.dense ? 2 : 1;
+    m0->team_xs_last = a.xs;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
     m0->dec_timed = true;
@@ -1550,9 +1626,9 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
                               hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    if (fail) return set_error(LBC_E_HIP, "team decoder: a workgroup gave up waiting at a barrier (grid not resident?)");
     if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
-        fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d\n", T, S, a.plain, m0->team_fallbacks);
+        fprintf(stderr, "[lbic] team decode: T=%d S=%d xs=%d W=%d plain=%d reruns=%d\n", T, S, a.xs, a.W, a.plain,
+                m0->team_fallbacks);
     for (int t = 0; t < T; ++t)
         if ((rc = check_status(ms[t], (size_t)n_img, s))) return rc;
     return LBC_OK;
@@ -1572,6 +1648,14 @@ int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double*
 int lbc_team_mode(const lbc_model* m, int* mode) {
     if (!m || !mode) return set_error(LBC_E_ARG, "null argument");
     *mode = m->team_mode_last;
+    return LBC_OK;
+}
+
+int lbc_team_events(const lbc_model* m, int* sc1_reruns, int* timeouts, int* column_split) {
+    if (!m || !sc1_reruns || !timeouts || !column_split) return set_error(LBC_E_ARG, "null argument");
+    *sc1_reruns = m->team_fallbacks;
+    *timeouts = m->team_timeouts;
+    *column_split = m->team_xs_last;
     return LBC_OK;
 }
 

@@ -133,18 +133,31 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
                              // ranks over two XCDs; hand-offs write-through, plain = 0)
+    int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)
+                             // of EVERY XCD slot (S = 8 W); the workgroups of slot x compute only the column tiles
+                             // team_xs_cols(x) of every GEMM, so each XCD's L2 holds 1/8 of the weights, shared by the
+                             // workgroups of all teams on it; hand-offs write-through (plain = 0)
 };
-// the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
-__host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
-    const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
+// the team kernel's fast GEMM path (team_gemm_items) covers g for S workgroups sharing ntn column tiles (ntn < 0: all
+// of g's column tiles): what a split GEMM needs
+__host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S, int ntn = -1) {
+    const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4;
+    const int items = MT * (ntn < 0 ? (g.N + 15) >> 4 : ntn);
     const int ni = (items + S - 1) / S;
     return S % MT == 0 && L >= 4 && L <= 9 && ni <= TEAM_NI_MAX;
+}
+// column-split teams (TeamArgs::xs): the column tiles [nt0, nt0 + ntn) of a GEMM with NT column tiles that XCD slot x
+// computes (balanced; a slot may get none)
+__host__ __device__ inline void team_xs_cols(int NT, int x, int& nt0, int& ntn) {
+    nt0 = x * NT / TEAM_MAX;
+    ntn = (x + 1) * NT / TEAM_MAX - nt0;
 }
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
 size_t team_lds_bytes(const TeamArgs& a);   // k_dec_team's dynamic LDS for a launch
 int launch_dec_team(const TeamArgs& a, hipStream_t s);
-int team_blocks_per_cu();          // k_dec_team workgroups one CU holds (occupancy query; 0 on error)
+int team_blocks_per_cu(int dense, size_t lds);   // k_dec_team<dense> workgroups one CU holds at `lds` bytes of dynamic
+                                                // LDS (occupancy query; 0 on error)
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
 int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = k_gemm
 int launch_rans_decode(const RansArgs& a, hipStream_t s);

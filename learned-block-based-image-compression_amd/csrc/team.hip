@@ -38,20 +38,21 @@ __device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
 
 // K beyond the fast path (or more than two row tiles): each output tile (row tile mt, column tile nt) = item
 // i = nt * MT + mt, items rank, rank + S, ...; each item's slice in chunks of 8 k-blocks, no prefetch
-__device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt) {
+__device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn, float* red,
+                                               bool wt) {
     constexpr int CH = 8;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = g.K >> 4;
     const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
-    const int MT = (g.M + 15) >> 4, NT = (g.N + 15) >> 4, items = MT * NT;
+    const int MT = (g.M + 15) >> 4, items = MT * ntn;
     const BlkSrc blocks{nullptr, 1, 0, v, h};
     const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     const int el = threadIdx.x & 63, er = (threadIdx.x >> 6) & 3;
     int buf = 0;
     for (int it = rank; it < items; it += S) {
-        const int mt = it % MT, nt = it / MT;
+        const int mt = it % MT, nt = nt0 + it / MT;
         const int erow = min(mt * 16 + (el >> 4) * 4 + er, g.M - 1), ecol = min(nt * 16 + (el & 15), g.N - 1);
         const float bb = g.bias[ecol];
         const float xx = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
@@ -120,8 +121,8 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 }
 
 template <int L, bool EXACT, bool SQ>
-__device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int ni, float* red,
-                                                bool wt, int ph, int wy, unsigned long long* dts) {
+__device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
+                                                float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
     constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments
     constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
@@ -143,7 +144,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         for (int q = 0; q < NOMAX; ++q) {        // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
             const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NOMAX
             const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
-            const int nt = (rank + j * S) / MT;
+            const int nt = nt0 + (rank + j * S) / MT;
             const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
             bb[q] = g.bias[ecol];
             xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
@@ -153,7 +154,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
-            const int nt = (rank + j * S) / MT;
+            const int nt = nt0 + (rank + j * S) / MT;
 #pragma unroll
             for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
         };
@@ -216,31 +217,34 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         float vv = red[j * KSPLIT * 256 + ee];
 #pragma unroll
         for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
-        const int nt = (rank + j * S) / MT;
+        const int nt = nt0 + (rank + j * S) / MT;
         const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
         if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb[q], xx[q], wt);
     }
     dstamp(dts, 4, 0.f);
 }
 
-__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
-                                              int ph = 0, int wy = 0, unsigned long long* dts = nullptr) {
+// The output tiles of g this workgroup computes: rank `rank` of the S workgroups that share column tiles
+// [nt0, nt0 + ntn) (the whole GEMM, or -- column-split teams -- the range of this workgroup's XCD slot)
+__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn,
+                                              float* red, bool wt, int ph = 0, int wy = 0,
+                                              unsigned long long* dts = nullptr) {
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
     const bool exact = (nkb % KSPLIT) == 0;
-    const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
+    const int MT = (g.M + 15) >> 4, items = MT * ntn;
     const int ni = rank < items ? (items - rank + S - 1) / S : 0;
     if (ni == 0) return;
-    if (team_fast_path(g, S)) {
+    if (team_fast_path(g, S, ntn)) {
         switch (L * 2 + (exact ? 1 : 0)) {
-#define LBIC_N(L_)                                                                                     \
-    case L_ * 2 + 1:                                                                                   \
-        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);     \
-        else team_gemm_items<L_, true, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);              \
-        return;                                                                                        \
-    case L_ * 2:                                                                                       \
-        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);    \
-        else team_gemm_items<L_, false, false>(g, v, h, rank, S, ni, red, wt, ph, wy, dts);             \
+#define LBIC_N(L_)                                                                                          \
+    case L_ * 2 + 1:                                                                                        \
+        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);     \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);              \
+        return;                                                                                             \
+    case L_ * 2:                                                                                            \
+        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);    \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);             \
         return;
             LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
@@ -248,7 +252,7 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
         }
     }
     if (ph == 1) return;     // (the host splits a GEMM only where every workgroup takes the path above)
-    team_gemm_long(g, v, h, rank, S, red, wt);
+    team_gemm_long(g, v, h, rank, S, nt0, ntn, red, wt);
 }
 
 // The weight fragments of the first NIT items this workgroup computes in GEMM g (each wave: its K slice), requested
@@ -338,10 +342,26 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
     // spread 2 (at most four teams): team t = the workgroups of slots 2t and 2t + 1 (two XCDs), ranks interleaved
+    // xs (column-split): grid = 8 x T W; team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W) of every slot,
+    // rank = slot W + q % W; in a GEMM the W workgroups of slot x share the column tiles team_xs_cols(x)
     const int slot = blockIdx.x & 7;
-    const int team = ta.spread == 2 ? slot >> 1 : slot;
-    const int rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
+    int team, rank;
+    if (ta.xs) {
+        const int q = blockIdx.x >> 3;
+        team = q / ta.W;
+        rank = slot * ta.W + q % ta.W;
+    } else {
+        team = ta.spread == 2 ? slot >> 1 : slot;
+        rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
+    }
     if (team >= T || rank >= S) return;
+    // the GEMM tile share of this workgroup: rank grk of gS over the column tiles of its slot (xs) or of the GEMM
+    const int grk = ta.xs ? rank % ta.W : rank, gS = ta.xs ? ta.W : S;
+    auto cols = [&](const GemmArgs& g, int& nt0, int& ntn) {
+        const int NT = (g.N + 15) >> 4;
+        if (ta.xs) team_xs_cols(NT, slot, nt0, ntn);
+        else { nt0 = 0; ntn = NT; }
+    };
     unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
@@ -385,8 +405,11 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
             for (int op = 0; op < ta.nops; ++op) {
                 const int k = ta.opk[op];
                 if (k >= 0) {
-                    team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + k), v, h, rank, S, red, wt,
-                                  op == ta.split_op ? 2 : 0, ta.split_wy, samp ? ts + 64 + op * 8 : nullptr);
+                    const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + k);
+                    int nt0, ntn;
+                    cols(g, nt0, ntn);
+                    team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
+                                  samp ? ts + 64 + op * 8 : nullptr);
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
@@ -396,8 +419,10 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                             else rans_row_sparse<true>(R, lwin, r, lane, wt);
                         }
                     } else if (ta.split_op >= 0) {
-                        team_gemm_any(*(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]), v, h, rank, S, red,
-                                      wt, 1, ta.split_wy);
+                        const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
+                        int nt0, ntn;
+                        cols(g, nt0, ntn);
+                        team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy);
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
@@ -422,11 +447,11 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
 }
 
-int team_blocks_per_cu() {
+int team_blocks_per_cu(int dense, size_t lds) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_team<false>), 512, 0) !=
-        hipSuccess)
-        return 0;
+    const void* f = dense ? reinterpret_cast<const void*>(&k_dec_team<true>) : reinterpret_cast<const void*>(&k_dec_team<false>);
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 512, lds) != hipSuccess) return 0;
     return nb;
 }
 
@@ -448,7 +473,9 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
     if (a.spread != 1 && (a.spread != 2 || a.T > TEAM_MAX / 2 || a.S % 2 || a.plain))
         return set_error(LBC_E_ARG, "bad team spread");
-    const dim3 grid(8 * a.S / a.spread);
+    if (a.xs && (a.W < 1 || a.S != 8 * a.W || a.plain || a.spread != 1 || a.pf))
+        return set_error(LBC_E_ARG, "bad column-split team geometry");
+    const dim3 grid(a.xs ? 8 * a.T * a.W : 8 * a.S / a.spread);
     if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, grid, dim3(512), lds, s, a);
     else hipLaunchKernelGGL(k_dec_team<false>, grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");

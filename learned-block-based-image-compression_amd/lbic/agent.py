@@ -23,7 +23,7 @@ from . import dist as D
 from .layout import arrange_block_pixels_to_channel_dim, arrange_channel_dim_to_block_pixels
 from .metrics import ms_ssim
 from .model import BlockBasedImgCompLossyNetv9
-from .weights import load_reference_checkpoint, synth_state_dict
+from .weights import load_reference_checkpoint, rate_for_lambda, synth_state_dict
 
 IMG_EXT = (".png", ".jpg", ".jpeg", ".bmp", ".ppm")
 
@@ -97,9 +97,12 @@ class BlockBasedImgCompLossyAgent:
             self.logger.info("Loading checkpoint '{}'".format(path))
             self.model0.load_state_dict(load_reference_checkpoint(path), strict=True)
         else:
+            lam = self.lambda_[0] if isinstance(self.lambda_, (list, tuple)) else self.lambda_
+            rate = rate_for_lambda(lam)
             self.logger.warning("!!! No checkpoint exists at '{}'. Continuing with SYNTHETIC seeded weights "
-                                "(seed {}) -- rate/PSNR are not those of a trained model.".format(path, self.config.seed))
-            self.model0.load_state_dict(synth_state_dict(self.model0.arch, int(self.config.seed)))
+                                "(seed {}, '{}' operating point for lambda {}) -- rate/PSNR are not those of a trained "
+                                "model.".format(path, self.config.seed, rate, lam))
+            self.model0.load_state_dict(synth_state_dict(self.model0.arch, int(self.config.seed), rate=rate))
 
     def run(self):
         mode = self.config.mode

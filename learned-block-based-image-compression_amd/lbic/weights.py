@@ -42,12 +42,36 @@ LOW_Y_GAIN = 0.4
 LOW_SCALE_GAIN = 0.3
 LOW_MEAN_GAIN = 0.1
 LOW_SCALE_POW = 18.0
+# rate="mid" (the high-rate configs' published operating points, BASELINE.md: B8_highrate 1.63 bpp, B4_highrate 1.58
+# bpp): the "low" recipe (weak mean prediction, small scale-channel weights) with the latent gain and a constant
+# scale level set per architecture so that the seeded noise frames code near 1.6 bpp (MID_POINTS, calibrated by
+# tests/golden/tune_mid_rate.py with the CPU oracle's closed loop; other architectures use MID_DEFAULT)
+MID_POINTS = {   # (B, N, M) -> (latent gain, scale level); calibration bpp on a 64x64 noise frame
+    (8, 1152, 128): (1.0433, 0.3859),   # B8_highrate: 1.633 bpp (published 1.63)
+    (4, 512, 96): (0.6767, 0.2508),     # B4_highrate: 1.570 bpp (published 1.58)
+}
+MID_DEFAULT = (1.0, 0.3)
 
 
-def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high") -> Dict[str, np.ndarray]:
-    if rate not in ("high", "low"):
-        raise ValueError(f"rate must be 'high' or 'low', not {rate!r}")
-    low = rate == "low"
+def mid_point(arch: Arch):
+    """(latent gain, scale level) of rate="mid" for this architecture."""
+    return MID_POINTS.get((arch.B, arch.N, arch.M), MID_DEFAULT)
+
+
+def rate_for_lambda(lam: float) -> str:
+    """The synthetic operating point standing in for a config's trained model: the low-rate configs train at
+    lambda = 117.045, the high-rate ones at 11704.5 (configs/*.json)."""
+    return "low" if float(lam) < 1000.0 else "mid"
+
+
+def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high", mid=None) -> Dict[str, np.ndarray]:
+    """mid: (latent gain, scale level) overriding mid_point(arch) for rate="mid" (calibration only)."""
+    if rate not in ("high", "low", "mid"):
+        raise ValueError(f"rate must be 'high', 'mid' or 'low', not {rate!r}")
+    low = rate in ("low", "mid")
+    y_gain_low, s_mid = mid if mid is not None else mid_point(arch)
+    if rate == "low":
+        y_gain_low = LOW_Y_GAIN
     rng = np.random.default_rng(seed)
     out: Dict[str, np.ndarray] = {}
     convs = {c[0]: c for c in arch.conv_specs()}
@@ -58,7 +82,7 @@ def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high") -> Dict[s
             live = cin * (4 if (k == 3 and mtype == "A") else 5 if k == 3 else 1)
             w = rng.standard_normal(shape, dtype=np.float32) * np.float32(1.0 / math.sqrt(live))
             if mod == "prtr_forward3.5":
-                w *= np.float32(LOW_Y_GAIN if low else Y_GAIN)
+                w *= np.float32(y_gain_low if low else Y_GAIN)
             if mod == "prtr_inverse1":
                 w *= np.float32(YQ_GAIN)
             if mod == "prtr_inverse3.5":
@@ -70,7 +94,10 @@ def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high") -> Dict[s
         elif leaf == "bias":
             b = (rng.standard_normal(shape, dtype=np.float32) * np.float32(0.05))
             if mod == "get_meanscale.6":
-                if low:
+                if rate == "mid":
+                    t = np.arange(arch.M, dtype=np.float64) / max(arch.M - 1, 1)
+                    b[: arch.M] = (s_mid * np.exp(0.5 * (t - 0.5))).astype(np.float32)
+                elif low:
                     t = np.arange(arch.M, dtype=np.float64) / max(arch.M - 1, 1)
                     b[: arch.M] = np.exp(-2.6 + 3.6 * t ** LOW_SCALE_POW).astype(np.float32)
                 else:

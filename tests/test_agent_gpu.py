@@ -60,3 +60,49 @@ def test_main_validate_recu_reco_fast(tmp_path, monkeypatch, caplog):
     assert sum(l.startswith("Image ") and "RDLoss:" in l for l in lines) == 2
     assert any("Valid Epoch" in l for l in lines)
     assert any(l.startswith("avg_psnr") for l in lines)
+
+
+def test_main_reference_config_b8_lowrate_full_frame(tmp_path, monkeypatch, caplog):
+    """BASELINE config 1 through the reference's entry point: `python main.py configs/blkbsdimgcomp_B8_lowrate.json`
+    (the reference's config shipped verbatim, only valid_data redirected) on a 768x768 PNG of the full-frame fixture's
+    image; no checkpoint, so the agent loads the seeded synthetic weights at the config's operating point -- the very
+    weights and frame of tests/golden/frame_b8_lowrate.npz, the reference's own compress() closed loop.  The log line's
+    MSE / PSNR must be the fixture's, Enc-Dec.Mad 0.00 (agents/blkbsdimgcomp_agent.py:561-641)."""
+    import hashlib
+    import re
+    from PIL import Image
+    import main as lbic_main
+    from conftest import load_golden
+    g = load_golden("frame_b8_lowrate")
+    H, W = int(g["H"]), int(g["W"])
+    img = np.random.default_rng(int(g["image_seed"])).integers(0, 256, (1, 3, H, W), dtype=np.uint8)[0]
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["image_sha256"])
+    data = tmp_path / "kodak" / "test"
+    data.mkdir(parents=True)
+    Image.fromarray(np.ascontiguousarray(img.transpose(1, 2, 0))).save(data / "frame.png")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "learned-block-based-image-compression_amd", "configs", "blkbsdimgcomp_B8_lowrate.json")
+    cfg = json.load(open(src))
+    raw_keys = set(cfg)
+    cfg["valid_data"] = str(data)                          # the only override
+    assert set(cfg) == raw_keys and cfg["block_size"] == 8 and cfg["N"] == 768 and cfg["M"] == 96
+    p = tmp_path / "blkbsdimgcomp_B8_lowrate.json"
+    p.write_text(json.dumps(cfg))
+    monkeypatch.chdir(tmp_path)
+    with caplog.at_level(logging.INFO):
+        lbic_main.main([str(p)])
+    lines = [r.getMessage() for r in caplog.records]
+    imgs = [l for l in lines if l.startswith("Image ")]
+    assert len(imgs) == 1, lines
+    print(imgs[0])
+    m = re.search(r"MSE/PSNR:([\d.]+)/([\d.]+) Rate:([\d.]+) .*Enc/DecTime:([\d.]+)/([\d.]+) "
+                  r"Enc-Dec\.Mad/Max/Min:([\d.]+)/([\d.]+)/([\d.]+)", imgs[0])
+    assert m, imgs[0]
+    mse, psnr, rate = float(m.group(1)), float(m.group(2)), float(m.group(3))
+    psnr_ref = float(g["psnr_db"])
+    assert abs(psnr - psnr_ref) <= 0.005 + 1e-9, (psnr, psnr_ref)             # the line prints 2 decimals
+    assert abs(mse - 10 ** (-psnr_ref / 10)) <= 5e-6 + 1e-9, (mse, 10 ** (-psnr_ref / 10))   # 5 decimals
+    est_ref = float(g["bits_per_block"].sum()) / (H * W)
+    assert abs(rate - est_ref) <= 0.05 * est_ref, (rate, est_ref)            # actual rANS bytes vs the estimate
+    assert m.group(6) == "0.00" and m.group(7) == "0.00"
+    assert any("'low' operating point" in l for l in lines)

@@ -5,7 +5,8 @@
   config's operating point).  A full frame cannot be tie-screened, so the fixture lists the latents whose
   rounding / scale-table margins are below 1e-4; symbols and indexes must be bit-exact everywhere else (the
   test reports the mismatch count), reconstructions within 1e-5 relative (|dz| <= 1e-5 * max|z_ref|),
-  PSNR and estimated bpp within 1e-5 relative, and decode(encode) bit-exact.
+  PSNR within 1e-5 and estimated bpp within 1e-4 relative, and decode(encode) bit-exact -- all of which still hold
+  (and are asserted) when only scale indexes flip at listed near ties, since zhat depends on the symbols alone.
 * B8_highrate at 768x512 (the Kodak frame size), B4_highrate at 768x768 and B16_lowrate at 2048x2048: the
   reference-format round trip decode(encode) bit-exact on the GPU, and sampled blocks recomputed by the CPU
   oracle from the GPU's own reconstruction (teacher forced): symbols / indexes equal wherever the margins
@@ -52,29 +53,36 @@ def test_full_frame_b8_lowrate_vs_reference():
     bad_i = np.nonzero(idx != ref_idx)[0]
     print(f"full frame: {bad_s.size} symbol / {bad_i.size} index mismatches of {sym.size}; "
           f"near ties (<1e-4) in the fixture: {g['near_tie_symbols'].size} symbols, {g['near_tie_indexes'].size} indexes")
-    if bad_s.size or bad_i.size:
-        # a flip is allowed only at a recorded near tie, and then only from the first flipped block on (the
-        # closed loop carries the different reconstruction forward)
-        first = min(([int(bad_s.min())] if bad_s.size else []) + ([int(bad_i.min())] if bad_i.size else []))
-        assert first in set(g["near_tie_symbols"].tolist()) | set(g["near_tie_indexes"].tolist()), \
-            f"first mismatch at latent {first} is not a near tie"
-        print(f"closed loop diverged after the near tie at latent {first} (block {first // arch.M})")
+    ties = set(g["near_tie_symbols"].tolist()) | set(g["near_tie_indexes"].tolist())
+    # a flip is allowed only at a recorded near tie.  A SYMBOL flip changes the reconstruction, which the closed loop
+    # carries forward: from there on nothing can be compared.  An INDEX flip does not: zhat, PSNR and the estimated bits
+    # depend on the symbols, the means and the scales, not on which table codes a symbol -- so every assertion below
+    # still runs (and the decoder, which derives the same indexes as this encoder, must still reproduce zhat).
+    assert all(int(i) in ties for i in bad_i), f"index mismatches off the near ties: {sorted(set(bad_i.tolist()) - ties)}"
+    if bad_s.size:
+        first = int(bad_s.min())
+        assert first in ties, f"first symbol mismatch at latent {first} is not a near tie"
+        print(f"closed loop diverged after the symbol near tie at latent {first} (block {first // arch.M})")
         return
     zr = g["zhat_row_data"]
     dz = np.abs(z[g["zhat_rows"]] - zr).max()
-    assert dz <= REL * np.abs(zr).max(), f"zhat rows differ by {dz}"
     s = z.astype(np.float64).sum(-1)
-    assert np.abs(s - g["zhat_block_sum"]).max() <= REL * np.abs(z).sum(-1).max()
+    dsum = np.abs(s - g["zhat_block_sum"]).max()
     mse = np.mean((z.astype(np.float64) - xb) ** 2)
     psnr = -10 * np.log10(mse)
-    assert abs(psnr - float(g["psnr_db"])) <= REL * abs(float(g["psnr_db"]))
     bits = r["bits"][0].cpu().numpy().astype(np.float64).reshape(-1, arch.M).sum(-1)
     est, est_ref = bits.sum() / (H * W), g["bits_per_block"].sum() / (H * W)
-    print(f"full frame: PSNR {psnr:.5f} dB (ref {float(g['psnr_db']):.5f}), estimated bpp {est:.6f} (ref {est_ref:.6f}), "
-          f"max |dzhat| rows {dz:.2e}")
+    print(f"full frame vs reference: max |dzhat| rows {dz:.3e} (bar {REL * np.abs(zr).max():.3e}), block sums "
+          f"{dsum:.3e}, PSNR {psnr:.6f} dB (ref {float(g['psnr_db']):.6f}, rel {abs(psnr - float(g['psnr_db'])) / float(g['psnr_db']):.2e}), "
+          f"estimated bpp {est:.7f} (ref {est_ref:.7f}, rel {abs(est - est_ref) / est_ref:.2e})")
+    assert dz <= REL * np.abs(zr).max(), f"zhat rows differ by {dz}"
+    assert dsum <= REL * np.abs(z).sum(-1).max()
+    assert abs(psnr - float(g["psnr_db"])) <= REL * abs(float(g["psnr_db"]))
     assert abs(est - est_ref) <= 1e-4 * est_ref      # fp32 erfc/log2 of 884,736 latents summed
     streams = m.entropy_encode(r["symbols"], r["indexes"])
-    assert torch.equal(m.decompress_batch(streams, *xb.shape[:2]), r["zhat"])
+    zdec = m.decompress_batch(streams, *xb.shape[:2])
+    assert torch.equal(zdec, r["zhat"]), "full-frame decode != encode"
+    print("full frame: decode == encode (bit-exact)")
 
 
 def _teacher_forced(arch, sd, xb, zhat, sym, idx, blocks):

@@ -1,9 +1,8 @@
-"""The reference's own four configs (/root/reference/configs/*.json, read verbatim; only ``valid_data`` is
-redirected to a local PNG folder) through this repository's main.py: JSON parsing, the multi-lambda sweep
-(main.py:17-27 of the reference), process_config's experiment layout (utils/config.py:69-102), agent
-dispatch by name and the agent's construction up to the device check, which on this GPU-less host must be
-the loud "no GPU" error (no CPU fallback).  The same flow runs end to end on the GPU in
-tests/test_agent_gpu.py.  Skipped where /root/reference is absent (the GPU box).
+"""The reference's own four configs (shipped verbatim in learned-block-based-image-compression_amd/configs/; only
+``valid_data`` is redirected to a local PNG folder) through this repository's main.py: JSON parsing, the multi-lambda
+sweep (main.py:17-27 of the reference), process_config's experiment layout (utils/config.py:69-102), agent dispatch by
+name and the agent's construction up to the device check, which on this GPU-less host must be the loud "no GPU" error
+(no CPU fallback).  The same flow runs end to end on the GPU in tests/test_agent_gpu.py (B8_lowrate at 768x768).
 
 Also: bench.py's multi-GPU launcher and its per-image record gather (gloo, world size 2)."""
 import glob
@@ -13,10 +12,23 @@ import os
 import numpy as np
 import pytest
 
-REF_CONFIGS = sorted(glob.glob("/root/reference/configs/*.json"))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the reference's four configs, shipped verbatim (data) with the package
+REF_CONFIGS = sorted(glob.glob(os.path.join(ROOT, "learned-block-based-image-compression_amd", "configs", "*.json")))
 
 
-@pytest.mark.skipif(not REF_CONFIGS, reason="reference configs not present (GPU box)")
+def test_shipped_configs_are_verbatim():
+    """learned-block-based-image-compression_amd/configs/*.json are byte copies of the reference's configs/*.json
+    (compared where /root/reference is present, i.e. not on the GPU box)."""
+    assert len(REF_CONFIGS) == 4
+    ref_dir = "/root/reference/configs"
+    if not os.path.isdir(ref_dir):
+        pytest.skip("reference not present")
+    for p in REF_CONFIGS:
+        with open(p, "rb") as a, open(os.path.join(ref_dir, os.path.basename(p)), "rb") as b:
+            assert a.read() == b.read(), p
+
+
 @pytest.mark.parametrize("path", REF_CONFIGS, ids=[os.path.basename(p) for p in REF_CONFIGS])
 def test_reference_config_runs_through_main(path, tmp_path, monkeypatch):
     from PIL import Image

@@ -55,17 +55,23 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
     return ref, got, hs, st
 
 
+@pytest.mark.parametrize("xs", [0, 1])
 @pytest.mark.parametrize("name,T,n,shape", [
     ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
-    ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)),
+    ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)), ("b8_lowrate_2rows", 5, 48, (2, 9)),
 ])
-def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
+def test_team_equals_graph_decoder(name, T, n, shape, xs, monkeypatch):
+    """xs = 1: column-split teams (LBIC_TEAM_XS=1; every team spans the eight XCD slots, each slot a fixed eighth of
+    every GEMM's column tiles) -- the same results."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
+    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     g = load_golden("loop_" + name)
     Hb, Wb = shape or g["x"].shape[:2]
-    ref, got, _, _ = run_case(name, T, n, Hb, Wb, seed=T * 7 + n)
+    ref, got, hs, _ = run_case(name, T, n, Hb, Wb, seed=T * 7 + n)
     for t in range(T):
         assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    st = hs[0].team_stats()
+    assert st["mode"] == "team_sparse" and st["column_split"] == xs
 
 
 @pytest.mark.parametrize("name,T,n,shape", [("tiny_ks3311", 3, 5, (3, 4)), ("b8_lowrate_2rows", 4, 32, (2, 24))])
@@ -79,11 +85,13 @@ def test_team_write_through_mode(name, T, n, shape, monkeypatch):
         assert torch.equal(got[t], ref[t])
 
 
+@pytest.mark.parametrize("xs", [0, 1])
 @pytest.mark.parametrize("shape", [(1, 1), (1, 9), (7, 1), (3, 5), (2, 2)])
-def test_team_ragged_frames_ks3311(shape, monkeypatch):
+def test_team_ragged_frames_ks3311(shape, xs, monkeypatch):
     """One block, one row, one column, odd rectangles: the three column classes of the KS3311 step (layer-0 cache
     border cells at h = 0 and h = Wb - 1, both at once when Wb = 1)."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     ref, got, _, _ = run_case("tiny_ks3311", 3, 2, *shape, seed=sum(shape))
     for t in range(3):
         assert torch.equal(got[t], ref[t])
@@ -136,10 +144,12 @@ def test_team_small_teams(S, monkeypatch):
 @pytest.mark.parametrize("name,T,n,shape,scale", [
     ("tiny_ks3111", 3, 5, None, 0.05), ("tiny_ks3311", 8, 3, None, 0.05), ("b8_lowrate_2rows", 4, 32, (2, 24), 0.05),
     ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
-def test_team_dense_rans(name, T, n, shape, scale, monkeypatch):
+@pytest.mark.parametrize("xs", [0, 1])
+def test_team_dense_rans(name, T, n, shape, scale, xs, monkeypatch):
     """The dense rANS variant inside the team kernel (high rates; every workgroup stages the tables in its LDS once per
     launch, one wave per stream runs rans_row<true>): forced by LBIC_RANS_SPARSE=0 at the fixtures' low rates, and
     picked by rate (>= 1 bit per symbol, bypass escapes included) on high-amplitude batches."""
+    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     if scale < 1:
         monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
     else:
@@ -188,3 +198,39 @@ def test_team_stamps(monkeypatch):
     assert len(ts) == 2
     for row in ts:
         assert row[63] > row[62] > 0 and row[61] > row[60] > 0
+
+
+@pytest.mark.parametrize("xs", [0, 1])
+def test_team_barrier_timeout_falls_back(xs, monkeypatch):
+    """A team barrier that times out (forced: LBIC_TEAM_TMO=1 tick) ends the launch on every workgroup; the batches are
+    then decoded through lbc_decode one after another in the same call, with the same results, and the event is
+    counted (lbc_team_events) instead of failing the decode."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
+    _, hs0 = handles("b8_lowrate_2rows", 1)
+    before = hs0[0].team_stats()["timeout_fallbacks"]
+    monkeypatch.setenv("LBIC_TEAM_TMO", "1")
+    ref, got, hs, streams = run_case("b8_lowrate_2rows", 4, 32, 2, 12, seed=9)
+    for t in range(4):
+        assert torch.equal(got[t], ref[t])
+    st = hs[0].team_stats()
+    assert st["mode"] == "fallback" and st["timeout_fallbacks"] == before + 1, st
+    monkeypatch.delenv("LBIC_TEAM_TMO")
+    from lbic.model import decompress_teams
+    got = decompress_teams(hs, streams, 2, 12)
+    for t in range(4):
+        assert torch.equal(got[t], ref[t])
+    assert hs[0].team_stats()["mode"] == "team_sparse"
+
+
+def test_team_dense_two_workgroups_per_cu(monkeypatch):
+    """High rates (dense rANS, the ~70 KB table image in every workgroup's LDS) with LBC_OPT_TEAM_WG_PER_CU = 2: two
+    such workgroups do not fit one CU's LDS, so the launch must shrink to one per CU (occupancy query on the dense
+    instance with the launch's dynamic LDS) rather than start a grid that cannot be co-resident."""
+    monkeypatch.delenv("LBIC_RANS_SPARSE", raising=False)
+    monkeypatch.delenv("LBIC_TEAM_XS", raising=False)
+    ref, got, hs, _ = run_case("b8_lowrate_2rows", 8, 32, 2, 7, seed=21, scale=4.0, wpc=2)
+    for t in range(8):
+        assert torch.equal(got[t], ref[t])
+    st = hs[0].team_stats()
+    assert st["mode"] == "team_dense" and st["timeout_fallbacks"] == 0, st

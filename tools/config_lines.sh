@@ -9,11 +9,11 @@ O=$R/gpurun_out
 TAG=${1:-x}
 mkdir -p $O
 cd $R
-B="python3 -u bench.py --cpu-budget 0 --side-steps 0"
-timeout -k 10 300 $B --config B8_highrate --rate high --size 768 --height 512 --batch 3 --steps 12 --warmup 3 > $O/cfg3_shard_$TAG.log 2>&1
-timeout -k 10 300 $B --config B8_highrate --rate high --size 768 --height 512 --batch 24 --steps 8 --warmup 3 > $O/cfg3_all24_$TAG.log 2>&1
-timeout -k 10 400 $B --config B4_highrate --rate high --size 768 --batch 32 --steps 6 --warmup 3 > $O/cfg4_$TAG.log 2>&1
-timeout -k 10 400 $B --config B16_lowrate --rate low --size 2048 --batch 8 --steps 6 --warmup 3 > $O/cfg5_$TAG.log 2>&1
+B="python3 -u bench.py --cpu-budget 0 --side-steps 0 --per-image 0"
+timeout -k 10 300 $B --config B8_highrate --size 768 --height 512 --batch 3 --steps 12 --warmup 3 > $O/cfg3_shard_$TAG.log 2>&1
+timeout -k 10 300 $B --config B8_highrate --size 768 --height 512 --batch 24 --steps 8 --warmup 3 > $O/cfg3_all24_$TAG.log 2>&1
+timeout -k 10 400 $B --config B4_highrate --size 768 --batch 32 --steps 6 --warmup 3 > $O/cfg4_$TAG.log 2>&1
+timeout -k 10 400 $B --config B16_lowrate --size 2048 --batch 8 --steps 6 --warmup 3 > $O/cfg5_$TAG.log 2>&1
 for f in cfg3_shard cfg3_all24 cfg4 cfg5; do
   grep '^{' $O/${f}_$TAG.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$f', d['value'], d['unit'], d['ms_per_step'], d['phases_ms_per_step'], d['quality']['bpp'], d['quality']['enc_dec_bit_exact'])"
 done
