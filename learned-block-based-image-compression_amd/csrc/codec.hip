@@ -1418,7 +1418,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
     HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
-    if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned)))) return rc;
+    if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 2) * 32 * sizeof(unsigned)))) return rc;
     if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
     TeamArgs& a = m0->team_args;
     a = TeamArgs{};
@@ -1569,6 +1569,8 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     a.tmo = tmoe ? std::max(1ull, strtoull(tmoe, nullptr, 10)) : 100000000ull;
     const char* st = getenv("LBIC_TEAM_STAMPS");
     a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
+    const char* ale = getenv("LBIC_TEAM_ALIGN");   // cross-team step alignment (0 off, 1 one step of lag, 2 lockstep)
+    a.align = ale ? std::max(0, std::min(2, atoi(ale))) : 0;
     const char* pfe = getenv("LBIC_TEAM_PF");   // weight tiles of the next GEMM requested at each barrier (0..2)
     a.pf = pfe && !xs ? std::max(0, std::min(2, atoi(pfe))) : 0;
     a.sv = Hb / 2;
@@ -1592,7 +1594,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     unsigned fail = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if ((rc = reset())) return rc;
-        HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 1) * 32 * sizeof(unsigned), s));
+        HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 2) * 32 * sizeof(unsigned), s));
         if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 256 * sizeof(unsigned long long), s));
         HIPCHK(hipEventRecord(m0->ev[2], s));
         if ((rc = launch_dec_team(a, s))) return rc;

@@ -116,7 +116,8 @@ struct TeamArgs {
     int nops, NG, T, S, Hb, Wb;
     unsigned* sync;          // [T][32]: per team [0] arrival counter, [1] XCD census (one 128-byte line each), then
                              // [T * 32] the failure word (1 timeout, 2 a team spans XCDs) and [T * 32 + 1] the
-                             // census barrier; zeroed before every launch
+                             // census barrier, [(TEAM_MAX + 1) * 32] the alignment step counter; zeroed before every
+                             // launch
     int plain;               // 1: plain hand-off stores (needs every team on one XCD: checked in-kernel)
     int ni_max;              // most output tiles one workgroup computes in one GEMM of the step (LDS for partials)
     int split_op, split_wy;  // split_op >= 0: the GEMM after the rANS decode; its K slices w < split_wy (no y_qnt)
@@ -133,6 +134,8 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
                              // ranks over two XCDs; hand-offs write-through, plain = 0)
+    int align;               // cross-team step alignment (0 off; 1 teams at most one raster step apart; 2 lockstep):
+                             // a launch-wide step counter [(TEAM_MAX + 1) * 32] in `sync`
     int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)
                              // of EVERY XCD slot (S = 8 W); the workgroups of slot x compute only the column tiles
                              // team_xs_cols(x) of every GEMM, so each XCD's L2 holds 1/8 of the weights, shared by the

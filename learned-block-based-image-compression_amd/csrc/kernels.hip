@@ -33,11 +33,26 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin over the 8 XCDs,
     // so XCD (bid % 8) gets a contiguous run of row-major tiles and its L2 serves their shared A rows
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
-    if (g.swz) {
-        const int full = (gridDim.x * gridDim.y) & ~7;
-        if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    int n0, m0;
+    if ((g.swz & 15) == 2) {
+        // 2-D XCD partition (swz = 2 | RG << 4; the launcher picks RG x CG = 8 to minimise the fabric bytes
+        // M K CG + K N RG): XCD slot x = bid % 8 owns row-tile group x / CG and column-tile group x % CG, so each
+        // XCD fetches 1/RG of the A rows and 1/CG of the weights once instead of (1-D round-robin) all of one of them
+        const int RG = g.swz >> 4, CG = KSPLIT / RG;
+        const int MT = (g.M + BM - 1) / BM, NT = (g.N + BN - 1) / BN;
+        const int x = bid & 7, l = bid >> 3, rg = x / CG, cg = x % CG;
+        const int r0 = rg * MT / RG, r1 = (rg + 1) * MT / RG, c0 = cg * NT / CG, nc = (cg + 1) * NT / CG - c0;
+        if (nc <= 0 || l >= (r1 - r0) * nc) return;      // the grid is sized for the largest share
+        m0 = (r0 + l / nc) * BM;
+        n0 = (c0 + l % nc) * BN;
+    } else {
+        if (g.swz) {
+            const int full = (gridDim.x * gridDim.y) & ~7;
+            if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+        }
+        n0 = (bid % gridDim.x) * BN;
+        m0 = (bid / gridDim.x) * BM;
     }
-    const int n0 = (bid % gridDim.x) * BN, m0 = (bid / gridDim.x) * BM;
     const int q4 = (lane >> 4) * 4;
 
     stamp_start(g.ts);
@@ -239,7 +254,8 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
 }
 
 static int enc_swz() {   // LBIC_ENC_SWZ=1: XCD-aware tile order (off: with four workers' kernels interleaving on the
-                         // GPU, workgroups no longer land on XCDs in launch order; plain order 61.3 vs 60.6 Mpix/s)
+                         // GPU, workgroups no longer land on XCDs in launch order; plain order 61.3 vs 60.6 Mpix/s);
+                         // 2: the 2-D XCD partition of row and column tiles (k_gemm)
     const char* e = getenv("LBIC_ENC_SWZ");
     return e ? atoi(e) : 0;
 }
@@ -284,6 +300,24 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     GemmArgs gs = g;
     gs.swz = g_enc_swz;
+    if (g_enc_swz == 2) {
+        // RG x CG = 8 minimising M K CG + K N RG (fabric bytes: every XCD reads its row group's A and column group's W)
+        const int MT = (g.M + BM - 1) / BM, NT = (g.N + BN - 1) / BN;
+        int best = 1;
+        double bc = 1e300;
+        for (int RG = 1; RG <= 8; RG *= 2) {
+            const double c = (double)g.M * (8 / RG) + (double)g.N * RG;
+            if (c < bc && MT >= RG && NT >= 8 / RG) { bc = c; best = RG; }
+        }
+        const int CG = 8 / best;
+        int most = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int rg = x / CG, cg = x % CG;
+            most = std::max(most, ((rg + 1) * MT / best - rg * MT / best) * ((cg + 1) * NT / CG - cg * NT / CG));
+        }
+        gs.swz = 2 | (best << 4);
+        grid = dim3(8 * most, 1);
+    }
     hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, gs);
     return launch_status("k_gemm");
 }

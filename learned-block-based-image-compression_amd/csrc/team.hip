@@ -288,6 +288,30 @@ __device__ __forceinline__ void team_prefetch_any(const GemmArgs* g, int rank, i
     else team_prefetch<1>(*g, rank, S, sink);
 }
 
+// wait (one lane polls, relaxed, s_sleep between polls, bounded) until *c >= target; false: the launch failed
+__device__ __forceinline__ bool team_wait(unsigned* c, unsigned target, unsigned* fail, unsigned long long tmo,
+                                          int* sflag) {
+    if (threadIdx.x == 0) {
+        int f = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load((gptr<unsigned>)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                f = 1;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                __hip_atomic_store((gptr<unsigned>)fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sflag = f;
+    }
+    __syncthreads();
+    return *sflag == 0;
+}
+
 // team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
 // (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else).  pf: the next
 // GEMM, whose first weight tiles are requested after the arrival (team_prefetch)
@@ -442,6 +466,18 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
             }
             if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
             if (ts && v == ta.sv && h == ta.sh - 1 && threadIdx.x == 0) ts[60] = __builtin_amdgcn_s_memrealtime();
+            if (ta.align) {
+                // cross-team step alignment (column-split teams: the teams on an XCD read the same weight slice, which
+                // stays in its L2 only while they run the same operation at about the same time).  The team's rank 0
+                // counts the finished step on one launch-wide counter; every workgroup then waits until every team has
+                // finished step s + 1 - lag (align 2: lag 0, lockstep; align 1: lag 1, at most one step apart)
+                unsigned* gctr = ta.sync + (TEAM_MAX + 1) * 32;
+                const unsigned sidx = (unsigned)(v * ta.Wb + h);
+                if (rank == 0 && threadIdx.x == 0)
+                    __hip_atomic_fetch_add((gptr<unsigned>)gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned need = (unsigned)T * (sidx + (ta.align == 2 ? 1u : 0u));
+                if (need && !team_wait(gctr, need, fail, ta.tmo, &sflag)) return;
+            }
         }
     }
     if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
