@@ -116,6 +116,9 @@ def parse_args(argv=None):
                     help="team decoder geometry: 1 column-split teams (each team spans the 8 XCD slots, each slot a fixed "
                          "eighth of every GEMM's columns: the decoder weights stay L2-resident), 0 one XCD slot per team, "
                          "-1 the library default (LBIC_TEAM_XS)")
+    ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
+                    help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
+                         "still decoded as its own 32-frame batch)")
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
@@ -423,12 +426,26 @@ def main():
             dth = threading.Thread(target=team_decoder)
             dth.start()
             with ThreadPoolExecutor(max_workers=4) as ex:
-                for k in range(steps):
-                    r_ = compress_side(ph, frames_of(base + k))
-                    f_ = ex.submit(entropy_side, r_, fmt, ph)
-                    # only the last batch keeps its record (zhat, symbols) for the quality check
-                    dq.put((base + k, r_ if k == steps - 1 else None, f_))
-                    del r_
+                k = 0
+                while k < steps:
+                    g = min(args.enc_pass, steps - k)
+                    if args.enc_pass == 1 or (base + k) % 2:
+                        g = 1
+                        rs_ = [compress_side(ph, frames_of(base + k))]
+                    else:
+                        # batches k, k + 1 = frame sets 0, 1 (contiguous in xb_all): one wavefront pass.  An odd last
+                        # batch is coded in a two-batch pass as well (its partner's codes are dropped): the encoder
+                        # graph keeps one frame count, so no pass re-captures it
+                        rr_ = compress_side(ph, xb_all[:2 * n])
+                        rs_ = [{kk: (v[e * n:(e + 1) * n] if v is not None else None) for kk, v in rr_.items()}
+                               for e in range(g)]
+                        del rr_
+                    for e, r_ in enumerate(rs_):
+                        f_ = ex.submit(entropy_side, r_, fmt, ph)
+                        # only the last batch keeps its record (zhat, symbols) for the quality check
+                        dq.put((base + k + e, r_ if k + e == steps - 1 else None, f_))
+                    del rs_, r_
+                    k += g
                 dq.put(None)
                 dth.join()
             if errs:
@@ -553,6 +570,8 @@ def main():
 
     # warmup: every decoder handle builds its row graphs, then `warmup` batches through the pipeline
     scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
+    if args.team and args.enc_pass == 2:
+        compress_side(scratch, xb_all[:2 * n])       # the two-batch encoder graph (captured once)
     r0 = compress_side(scratch, frames_of(0))
     st0 = entropy_side(r0, "reference", scratch)
     if not args.team:
@@ -645,7 +664,8 @@ def main():
                                   f"{depth} pass(es) in flight beside the encoder"),
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
                    "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
-                   "decode_passes_in_flight": args.team or args.workers or depth, "frames_per_encode_pass": n,
+                   "decode_passes_in_flight": args.team or args.workers or depth,
+                   "frames_per_encode_pass": n * (args.enc_pass if args.team else 1),
                    "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
                                 f"helper threads; every {args.team} encoded batches are decoded by ONE persistent "
                                 "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "
