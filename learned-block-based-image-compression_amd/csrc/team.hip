@@ -139,17 +139,22 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     const int nout = ni * 256;
     dstamp(dts, 0, 0.f);
     float bb[NOMAX], xx[NOMAX];
-    if (ph != 1) {
+    auto epi_operands = [&]() {
+        if (ph != 1) {
 #pragma unroll
-        for (int q = 0; q < NOMAX; ++q) {        // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
-            const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NOMAX
-            const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
-            const int nt = nt0 + (rank + j * S) / MT;
-            const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
-            bb[q] = g.bias[ecol];
-            xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+            for (int q = 0; q < NOMAX; ++q) {    // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
+                const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NOMAX
+                const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
+                const int nt = nt0 + (rank + j * S) / MT;
+                const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
+                bb[q] = g.bias[ecol];
+                xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+            }
         }
-    }
+    };
+#ifdef LBIC_TEAM_WFIRST
+    epi_operands();    // (round-2 order, a build variant for A/B runs: epilogue operands, item 0's weights, then A)
+#endif
     dstamp(dts, 5, 0.f);
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
@@ -176,6 +181,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             if (j == 0) dstamp(dts, 2, acc[0]);
             if (j == ni - 1) dstamp(dts, 3, acc[0]);
         };
+#ifdef LBIC_TEAM_WFIRST
         issue(0, w0);
         dstamp(dts, 6, 0.f);
         {
@@ -186,6 +192,27 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 #pragma unroll
             for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
         }
+#else
+        // A first, then item 0's (A, W) fragments interleaved k-block by k-block: loads return in issue order, so the
+        // chain's first MFMA waits for one pair instead of all of the item's weights, and the A rows (the operand
+        // that depends on the barrier just crossed) are not queued behind the CU's weight requests.  The epilogue's
+        // operands (needed last) are requested after them.
+        {
+            const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
+            SRow rw;
+            small_offsets(g, bk, lane, rw);
+            dstamp(dts, 7, 0.f);
+            const int nt = nt0 + rank / MT;
+#pragma unroll
+            for (int c = 0; c < LL; ++c) {
+                const int kb = min(kb0 + c, nkb - 1);
+                a[c] = small_a_sc1(rw, kb);
+                w0[c] = Wt[((long)kb * g.NB16 + nt) * 64];
+            }
+        }
+        dstamp(dts, 6, 0.f);
+        epi_operands();
+#endif
         dstamp(dts, 1, 0.f);
         // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
         // hit) so that no load sits behind a branch
@@ -206,6 +233,11 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             }
         }
     }
+#ifndef LBIC_TEAM_WFIRST
+    else {
+        epi_operands();    // waves with no chain in this phase still finish outputs
+    }
+#endif
     if (ph == 1) return;
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
