@@ -40,10 +40,11 @@ __device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
 }
 
 // K beyond the fast path (or more than two row tiles): each output tile (row tile mt, column tile nt) = item
-// i = nt * MT + mt, items rank, rank + S, ...; each item's slice in chunks of 8 k-blocks, no prefetch
+// i = nt * MT + mt, items rank, rank + S, ...; each item's slice in chunks of CH k-blocks, double-buffered: chunk c + 1's
+// fragments are requested before chunk c's MFMAs (the KS3311 context layer 1, K = 5 C1, streams 8-67 k-blocks per slice)
 __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn, float* red,
                                                bool wt) {
-    constexpr int CH = 8;
+    constexpr int CH = 4;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = g.K >> 4;
@@ -63,15 +64,18 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
         SRow rw;
         small_offsets(g, bk, lane, rw);
         f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        for (int c0 = kb0; c0 < kb1; c0 += CH) {
-            const int cn = min(CH, kb1 - c0);
-            f4 a[CH], w[CH];
+        f4 a0[CH], w0[CH], a1[CH], w1[CH];
+        // clamped, unconditional loads (a block past the slice re-reads a valid one; its MFMAs are discarded below)
+        auto load = [&](int c0, f4 (&a)[CH], f4 (&w)[CH]) {
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 const int kb = min(c0 + c, nkb - 1);
                 w[c] = Wt[((long)kb * g.NB16 + nt) * 64];
                 a[c] = small_a_sc1(rw, kb);
             }
+        };
+        auto mma = [&](int c0, f4 (&a)[CH], f4 (&w)[CH]) {
+            __builtin_amdgcn_sched_barrier(0);   // the next chunk's requests stay above this chunk's MFMAs
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 f4 av = a[c];
@@ -79,8 +83,20 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
                 f4 t = acc;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-                acc = c < cn ? t : acc;
+                acc = c0 + c < kb1 ? t : acc;
             }
+        };
+        int c0 = kb0;
+        load(c0, a0, w0);
+        for (;;) {
+            load(c0 + CH, a1, w1);
+            mma(c0, a0, w0);
+            c0 += CH;
+            if (c0 >= kb1) break;
+            load(c0 + CH, a0, w0);
+            mma(c0, a1, w1);
+            c0 += CH;
+            if (c0 >= kb1) break;
         }
         float* rb = red + buf * (KSPLIT * 256);
         buf ^= 1;

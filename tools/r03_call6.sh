@@ -7,6 +7,10 @@ O=$R/gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
 cd $R
+timeout -k 10 600 python -u -m pytest tests -v -m gpu -k "team" --timeout 300 --timeout-method thread > $O/r03_tests_v6.log 2>&1
+rc=$?
+tail -3 $O/r03_tests_v6.log
+[ $rc -eq 0 ] || { echo "pytest rc=$rc: stopping"; grep -E "FAILED|Error" $O/r03_tests_v6.log | head; exit $rc; }
 B="python3 -u bench.py --cpu-budget 0 --side-steps 0 --per-image 0"
 for cfg in "0 0" "1 0" "1 2"; do
   set -- $cfg
