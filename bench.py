@@ -189,7 +189,10 @@ def cpu_baseline(arch, sd, H, W, budget_s):
                        f"of the first {rows_all} of {Hb} block rows of one {H}x{W} frame at {threads_all} threads "
                        f"({t_all:.1f} s); per-block cost is content-independent",
                 single_thread=dict(value=round(v1, 6), cores=1, rows=rows1, seconds=round(t1_, 2)),
-                cpu_model=model, nproc=nproc)
+                cpu_model=model, nproc=nproc,
+                threads_note=("all threads this job is granted: OMP_NUM_THREADS (the host's CPU share of one GPU's job; "
+                              "nproc counts the whole machine)" if os.environ.get("OMP_NUM_THREADS") else
+                              "all nproc threads"))
 
 
 def main():
