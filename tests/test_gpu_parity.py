@@ -385,3 +385,36 @@ def test_sibling_handles_share_weights():
     assert torch.equal(sib.compress_batch(x)["symbols"], r["symbols"])
     del m
     assert torch.equal(sib.decompress_batch(streams, *g["x"].shape[:2]), r["zhat"])
+
+
+def test_failed_finalize_keeps_the_working_weights():
+    """lbc_finalize packs into a new weight set and installs it only when every layer packed: on a sibling
+    (no host tensors) it fails and the sibling keeps coding with its shared weights; a re-finalize of the source with a
+    new state dict rebuilds the team program (keyed on the packed set's id, not on reusable addresses)."""
+    import ctypes
+    from lbic import _lib
+    from lbic.model import BlockBasedImgCompLossyNetv9, decompress_teams
+    g = load_golden("loop_tiny_ks3311")
+    arch = golden_arch(g)
+    cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
+    m = BlockBasedImgCompLossyNetv9(cfg)
+    m.load_state_dict(synth_state_dict(arch, int(g["weight_seed"])))
+    m.update(force=True)
+    sib = m.sibling()
+    x = torch.from_numpy(g["x"])[None].cuda()
+    r = m.compress_batch(x)
+    assert _lib.lib().lbc_finalize(sib._h) != 0              # a sibling holds no host tensors: packing fails ...
+    rs = sib.compress_batch(x)                                # ... and it still codes with the shared weights
+    assert torch.equal(rs["symbols"], r["symbols"]) and torch.equal(rs["zhat"], r["zhat"])
+    streams = m.entropy_encode(r["symbols"], r["indexes"])
+    Hb, Wb = g["x"].shape[:2]
+    z1 = decompress_teams([m, sib], [streams, streams], Hb, Wb)
+    assert torch.equal(z1[0], r["zhat"]) and torch.equal(z1[1], r["zhat"])
+    # re-finalize the source with other weights: the recorded team program must follow the new weight set
+    m.load_state_dict(synth_state_dict(arch, int(g["weight_seed"]) + 3))
+    m.update(force=True)
+    r2 = m.compress_batch(x)
+    s2 = m.entropy_encode(r2["symbols"], r2["indexes"])
+    sib2 = m.sibling()
+    z2 = decompress_teams([m, sib2], [s2, s2], Hb, Wb)
+    assert torch.equal(z2[0], r2["zhat"]) and torch.equal(z2[1], r2["zhat"])
