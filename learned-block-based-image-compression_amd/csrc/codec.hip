@@ -1573,9 +1573,6 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     a.align = ale ? std::max(0, std::min(2, atoi(ale))) : 0;
     const char* pfe = getenv("LBIC_TEAM_PF");   // weight tiles of the next GEMM requested at each barrier (0..2)
     a.pf = pfe && !xs ? std::max(0, std::min(2, atoi(pfe))) : 0;
-    const char* xpe = getenv("LBIC_TEAM_XPF");   // next GEMM's item-0 weights into registers at each barrier
-    a.xpf = xpe ? (atoi(xpe) != 0) : 0;
-    if (a.xpf) a.pf = 0;
     a.sv = Hb / 2;
     a.sh = Wb / 2;
     auto reset = [&]() -> int {

@@ -134,8 +134,6 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
                              // ranks over two XCDs; hand-offs write-through, plain = 0)
-    int xpf;                 // 1: item 0's weight fragments of the next GEMM are requested into registers right after
-                             // each team-barrier arrival and used by that GEMM (team_prefetch_regs); excludes pf
     int align;               // cross-team step alignment (0 off; 1 teams at most one raster step apart; 2 lockstep):
                              // a launch-wide step counter [(TEAM_MAX + 1) * 32] in `sync`
     int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)

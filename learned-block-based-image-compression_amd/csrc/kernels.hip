@@ -23,9 +23,7 @@ namespace lbic {
 // is multiplied, so a slice of K costs about one memory round trip instead of one per k-block.
 // OCC: minimum waves per SIMD the register allocation must allow (1 = no constraint).  The team decoder keeps
 // 256 of each SIMD's 512 VGPRs while it runs, so the encoder's residency beside it is (512 - 256) / its VGPRs.
-// NB: chunk buffers in the k-loop (2: chunk c + 1 in flight while chunk c is multiplied; 3 / 4: two / three chunks ahead,
-// with unconditional, clamped loads past the slice end)
-template <int BM, int BN, int NW, int CH, int OCC = 1, int NB = 2>
+template <int BM, int BN, int NW, int CH, int OCC = 1>
 __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     constexpr int MS = BM / 16, NS = BN / 16, SPW = KSPLIT / NW;
     extern __shared__ __attribute__((aligned(16))) float red[];
@@ -107,55 +105,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
         };
         int kb = kb0;
         load_chunk(kb, fa);
-        if constexpr (NB == 2) {
-            while (kb < kb1) {               // two named buffers, statically indexed (no scratch)
-                if (kb + CH < kb1) load_chunk(kb + CH, fb);
-                mma_chunk(kb, fa);
-                kb += CH;
-                if (kb >= kb1) break;
-                if (kb + CH < kb1) load_chunk(kb + CH, fa);
-                mma_chunk(kb, fb);
-                kb += CH;
-            }
-        } else if constexpr (NB == 3) {
-            Frag<MS, NS> fc[CH];
-            load_chunk(kb + CH, fb);
-            for (;;) {                       // three named buffers: two chunks in flight behind the one multiplied
-                load_chunk(kb + 2 * CH, fc);
-                mma_chunk(kb, fa);
-                kb += CH;
-                if (kb >= kb1) break;
-                load_chunk(kb + 2 * CH, fa);
-                mma_chunk(kb, fb);
-                kb += CH;
-                if (kb >= kb1) break;
-                load_chunk(kb + 2 * CH, fb);
-                mma_chunk(kb, fc);
-                kb += CH;
-                if (kb >= kb1) break;
-            }
-        } else {
-            Frag<MS, NS> fc[CH], fd[CH];
-            load_chunk(kb + CH, fb);
-            load_chunk(kb + 2 * CH, fc);
-            for (;;) {                       // four named buffers: three chunks in flight
-                load_chunk(kb + 3 * CH, fd);
-                mma_chunk(kb, fa);
-                kb += CH;
-                if (kb >= kb1) break;
-                load_chunk(kb + 3 * CH, fa);
-                mma_chunk(kb, fb);
-                kb += CH;
-                if (kb >= kb1) break;
-                load_chunk(kb + 3 * CH, fb);
-                mma_chunk(kb, fc);
-                kb += CH;
-                if (kb >= kb1) break;
-                load_chunk(kb + 3 * CH, fc);
-                mma_chunk(kb, fd);
-                kb += CH;
-                if (kb >= kb1) break;
-            }
+        while (kb < kb1) {               // two named buffers, statically indexed (no scratch)
+            if (kb + CH < kb1) load_chunk(kb + CH, fb);
+            mma_chunk(kb, fa);
+            kb += CH;
+            if (kb >= kb1) break;
+            if (kb + CH < kb1) load_chunk(kb + CH, fa);
+            mma_chunk(kb, fb);
+            kb += CH;
         }
     }
 
@@ -330,12 +287,12 @@ static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B 
 }
 static const int g_exact = exact_on();
 
-template <int BM, int BN, int NW, int CH, int OCC = 1, int NB = 2>
+template <int BM, int BN, int NW, int CH, int OCC = 1>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "LDS request above 160 KB");
     static const bool attr = [] {     // once per instantiation (thread-safe static initialisation)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH, OCC, NB>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH, OCC>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -361,7 +318,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
         gs.swz = 2 | (best << 4);
         grid = dim3(8 * most, 1);
     }
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC, NB>), grid, dim3(NW * 64), lds, s, gs);
+    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, gs);
     return launch_status("k_gemm");
 }
 
@@ -456,10 +413,6 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         case 12: return launch_cfg<16, 64, 8, 1, 1>(g, s);
         case 13: return launch_cfg<32, 32, 8, 1, 1>(g, s);
         case 15: return launch_cfg<16, 32, 4, 2>(g, s);
-        case 16: return launch_cfg<16, 32, 8, 1, 1, 3>(g, s);   // two k-blocks in flight per wave
-        case 17: return launch_cfg<16, 32, 8, 1, 1, 4>(g, s);   // three
-        case 18: return launch_cfg<32, 32, 8, 1, 1, 3>(g, s);
-        case 19: return launch_cfg<16, 64, 8, 1, 1, 3>(g, s);
         default: return launch_cfg<16, 32, 8, 1>(g, s);    // 0 and 7
     }
 }

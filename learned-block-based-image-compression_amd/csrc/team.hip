@@ -21,9 +21,6 @@ namespace lbic {
 // GEMM arithmetic per output element is k_gemm_s's (KSPLIT slices, the same MFMA chains, the slice-ordered sum,
 // the shared epilogue): results are bit-identical to the graph decoder's.
 
-// cross-operation register prefetch (TeamArgs::xpf, team_prefetch_regs): the first k-blocks of item 0's K slice
-constexpr int TEAM_PRE = 4;
-
 // A fragment of k-block kb through an sc1 (L1-bypassing) buffer load; byte offsets < 4 GB (host-checked)
 __device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
     const int k = kb << 4;
@@ -141,8 +138,7 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 
 template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
-                                                float* red, bool wt, int ph, int wy, unsigned long long* dts,
-                                                f4* wpre, bool pre) {
+                                                float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
     constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments
     constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
@@ -173,12 +169,12 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     dstamp(dts, 5, 0.f);
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
-        auto issue = [&](int j, f4* w) {
+        auto issue = [&](int j, f4 (&w)[LL]) {
             const int nt = nt0 + (rank + j * S) / MT;
 #pragma unroll
             for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
         };
-        auto chain = [&](int j, f4* w) {
+        auto chain = [&](int j, f4 (&w)[LL]) {
             __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
             f4 acc = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -196,14 +192,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             if (j == 0) dstamp(dts, 2, acc[0]);
             if (j == ni - 1) dstamp(dts, 3, acc[0]);
         };
-        if (pre) {      // item 0's first TEAM_PRE fragments were requested before the barrier (team_prefetch_regs)
-            const int nt = nt0 + rank / MT;
-#pragma unroll
-            for (int c = 0; c < LL; ++c)
-                w0[c] = c < TEAM_PRE ? wpre[c < TEAM_PRE ? c : 0] : Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-        } else {
-            issue(0, w0);
-        }
+        issue(0, w0);
         dstamp(dts, 6, 0.f);
         {
             const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
@@ -254,8 +243,8 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 // The output tiles of g this workgroup computes: rank `rank` of the S workgroups that share column tiles
 // [nt0, nt0 + ntn) (the whole GEMM, or -- column-split teams -- the range of this workgroup's XCD slot)
 __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn,
-                                              float* red, bool wt, int ph, int wy, unsigned long long* dts, f4* wpre,
-                                              bool pre) {
+                                              float* red, bool wt, int ph = 0, int wy = 0,
+                                              unsigned long long* dts = nullptr) {
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
     const bool exact = (nkb % KSPLIT) == 0;
@@ -266,12 +255,12 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                          \
     case L_ * 2 + 1:                                                                                        \
-        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wpre, pre); \
-        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wpre, pre);          \
+        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);          \
         return;                                                                                             \
     case L_ * 2:                                                                                            \
-        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wpre, pre); \
-        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wpre, pre);         \
+        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);         \
         return;
             LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
@@ -309,28 +298,6 @@ __device__ __forceinline__ void team_prefetch(const GemmArgs& g, int rank, int S
     if (lane == 0) sink[wave] = s;
 }
 
-// Cross-operation register prefetch (TeamArgs::xpf): the weight fragments of item 0 of the NEXT GEMM (each wave: its K
-// slice, TEAM_PRE fragments, clamped to the slice's last k-block) requested right after this workgroup's arrival at the
-// team barrier, into registers the GEMM then uses as its first item's W operand (team_gemm_items, pre).  The loads stay
-// in flight through the poll and the closing barrier (which waits for LDS only); the chain waits for them where it
-// uses them.  Weights are read-only: no ordering against the barrier is needed.  True when issued.
-// The loads are issued unconditionally (at a valid address when g does not qualify), so wpre is written at every
-// barrier and its live range ends at the GEMM after it (a conditional write would keep it live around the whole loop).
-__device__ __forceinline__ bool team_prefetch_regs(const GemmArgs& g, int rank, int S, int nt0, int ntn, f4* wpre) {
-    const int MT = (g.M + 15) >> 4;
-    const bool ok = team_fast_path(g, S, ntn) && rank < MT * ntn;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nkb = g.K >> 4;
-    const int kb0 = wave * nkb / KSPLIT;
-    const int last = min(kb0 + nkb / KSPLIT, nkb - 1);     // the slice's LL-th k-block (clamped as issue() does)
-    const int nt = min(nt0 + rank / MT, ((g.N + 15) >> 4) - 1);
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-#pragma unroll
-    for (int c = 0; c < TEAM_PRE; ++c) wpre[c] = Wt[((long)min(kb0 + c, last) * g.NB16 + nt) * 64];
-    return ok;
-}
-
 __device__ __forceinline__ void team_prefetch_any(const GemmArgs* g, int rank, int S, int nit, float* sink) {
     if (!g || rank >= (((g->M + 15) >> 4) * ((g->N + 15) >> 4))) return;
     if (nit >= 2) team_prefetch<2>(*g, rank, S, sink);
@@ -359,14 +326,6 @@ __device__ __forceinline__ bool team_wait(unsigned* c, unsigned target, unsigned
     }
     __syncthreads();
     return *sflag == 0;
-}
-
-// the arrival half of team_sync: every wave's stores drained, one agent-scope arrival per workgroup
-__device__ __forceinline__ void team_arrive(unsigned* ctr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
@@ -409,7 +368,7 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch.
 // DENSE (TeamArgs::dense): the high-rate instance, tables staged in LDS and rans_row<true>; a separate instance so the
 // low-rate one keeps its register allocation.
-template <bool DENSE, bool XPF>
+template <bool DENSE>
 __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
     // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
@@ -479,8 +438,6 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
             return;
         }
     }
-    f4 wpre[TEAM_PRE];         // xpf: item 0's weight fragments of the next GEMM, requested at the barrier in front of it
-    bool have_pre = false;
     for (int v = 0; v < ta.Hb; ++v) {
         for (int h = 0; h < ta.Wb; ++h) {
             const int cls = h == 0 ? 0 : h == ta.Wb - 1 ? 2 : 1;
@@ -492,7 +449,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                     int nt0, ntn;
                     cols(g, nt0, ntn);
                     team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
-                                  samp ? ts + 64 + op * 8 : nullptr, wpre, XPF && have_pre);
+                                  samp ? ts + 64 + op * 8 : nullptr);
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
@@ -505,13 +462,13 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
                         int nt0, ntn;
                         cols(g, nt0, ntn);
-                        team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy, nullptr, wpre, false);
+                        team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy);
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
                 target += S;
                 const GemmArgs* nx = nullptr;
-                if (ta.pf || XPF) {     // the GEMM after this barrier (the next step's first at the step's end)
+                if (ta.pf) {     // the GEMM after this barrier (the next step's first at the step's end)
                     int nop = op + 1, ncls = cls;
                     if (nop == ta.nops) {
                         nop = 0;
@@ -520,19 +477,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                     }
                     if (ta.opk[nop] >= 0) nx = (const GemmArgs*)(G + ncls * ta.NG + ta.opk[nop]);
                 }
-                if constexpr (XPF) {
-                    // arrive, request the next GEMM's item-0 weights into wpre, then wait (team_sync split in two)
-                    team_arrive(ctr);
-                    const int nk = ta.opk[op + 1 == ta.nops ? 0 : op + 1];
-                    const GemmArgs& gn = *(nx ? nx : (const GemmArgs*)(G + (nk >= 0 ? nk : 0)));
-                    int nt0, ntn;
-                    cols(gn, nt0, ntn);
-                    have_pre = team_prefetch_regs(gn, grk, gS, nt0, ntn, wpre) && nx;
-                    if (!team_wait(ctr, target, fail, ta.tmo, &sflag)) return;
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the poll
-                } else if (!team_sync(ctr, target, fail, ta.tmo, &sflag, nx, rank, S, ta.pf, sink)) {
-                    return;
-                }
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag, nx, rank, S, ta.pf, sink)) return;
                 if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
             }
             if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
@@ -554,15 +499,13 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <bool D, bool X>
-static const void* team_fn() { return reinterpret_cast<const void*>(&k_dec_team<D, X>); }
-static const void* team_instance(int dense, int xpf) {
-    return dense ? (xpf ? team_fn<true, true>() : team_fn<true, false>()) : (xpf ? team_fn<false, true>() : team_fn<false, false>());
+static const void* team_instance(int dense) {
+    return dense ? reinterpret_cast<const void*>(&k_dec_team<true>) : reinterpret_cast<const void*>(&k_dec_team<false>);
 }
 
 int team_blocks_per_cu(int dense, size_t lds) {
     int nb = 0;
-    const void* f = team_instance(dense, 0);
+    const void* f = team_instance(dense);
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 512, lds) != hipSuccess) return 0;
     return nb;
@@ -578,8 +521,7 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
     static const bool attr = [] {
         for (int d = 0; d < 2; ++d)
-            for (int x = 0; x < 2; ++x)
-                (void)hipFuncSetAttribute(team_instance(d, x), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute(team_instance(d), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
@@ -590,13 +532,8 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.xs && (a.W < 1 || a.S != 8 * a.W || a.plain || a.spread != 1 || a.pf))
         return set_error(LBC_E_ARG, "bad column-split team geometry");
     const dim3 grid(a.xs ? 8 * a.T * a.W : 8 * a.S / a.spread);
-    if (a.dense) {
-        if (a.xpf) hipLaunchKernelGGL((k_dec_team<true, true>), grid, dim3(512), lds, s, a);
-        else hipLaunchKernelGGL((k_dec_team<true, false>), grid, dim3(512), lds, s, a);
-    } else {
-        if (a.xpf) hipLaunchKernelGGL((k_dec_team<false, true>), grid, dim3(512), lds, s, a);
-        else hipLaunchKernelGGL((k_dec_team<false, false>), grid, dim3(512), lds, s, a);
-    }
+    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_team<false>, grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

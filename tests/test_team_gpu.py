@@ -249,17 +249,3 @@ def test_team_step_alignment(xs, align, monkeypatch):
     for t in range(6):
         assert torch.equal(got[t], ref[t])
     assert hs[0].team_stats()["mode"] == "team_sparse"
-
-
-@pytest.mark.parametrize("xs", [0, 1])
-@pytest.mark.parametrize("name,T,n,shape,scale", [
-    ("b8_lowrate_2rows", 8, 32, (2, 12), 0.05), ("tiny_ks3311", 3, 5, (3, 5), 0.05), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
-def test_team_cross_op_prefetch(name, T, n, shape, scale, xs, monkeypatch):
-    """LBIC_TEAM_XPF=1: each workgroup requests the next GEMM's first weight fragments into registers right after its
-    barrier arrival, and that GEMM uses them -- the same results (both rANS variants, both team geometries)."""
-    monkeypatch.setenv("LBIC_TEAM_XPF", "1")
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
-    monkeypatch.delenv("LBIC_RANS_SPARSE", raising=False)
-    ref, got, hs, _ = run_case(name, T, n, *shape, seed=T + n, scale=scale)
-    for t in range(T):
-        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
