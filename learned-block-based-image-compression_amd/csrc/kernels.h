@@ -147,7 +147,7 @@ __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S, int ntn
     const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4;
     const int items = MT * (ntn < 0 ? (g.N + 15) >> 4 : ntn);
     const int ni = (items + S - 1) / S;
-    return S % MT == 0 && L >= 4 && L <= 9 && ni <= TEAM_NI_MAX;
+    return S % MT == 0 && L >= 1 && L <= 9 && ni <= TEAM_NI_MAX;
 }
 // column-split teams (TeamArgs::xs): the column tiles [nt0, nt0 + ntn) of a GEMM with NT column tiles that XCD slot x
 // computes (balanced; a slot may get none)
