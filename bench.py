@@ -257,8 +257,9 @@ def main():
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
-    s_copy = torch.cuda.Stream(dev)     # device-to-host copies of the codes (compress_side)
+    # (the copy stream of compress_side second: a stream sharing a hardware queue with the team decoder's would wait
+    # behind its second-long launches)
+    s_enc, s_copy, *s_decs = dedicated_streams(2 + ndec, dev)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
