@@ -257,9 +257,11 @@ def main():
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    # (the copy stream of compress_side second: a stream sharing a hardware queue with the team decoder's would wait
-    # behind its second-long launches)
-    s_enc, s_copy, *s_decs = dedicated_streams(2 + ndec, dev)
+    # (the team schedule decodes on one stream: only that one is created, so the copy stream of compress_side, created
+    # last, gets a hardware queue of its own -- one shared with the team decoder's would wait behind its second-long
+    # launches; the order encoder, decoder(s) is the measured one)
+    n_dec_streams = ndec if not args.team else (2 if args.gang > 1 else 1)
+    s_enc, *s_decs, s_copy = dedicated_streams(2 + n_dec_streams, dev)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
