@@ -119,7 +119,7 @@ def parse_args(argv=None):
     ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
                     help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
                          "still decoded as its own 32-frame batch)")
-    ap.add_argument("--narrow-codes", type=int, default=1, choices=(0, 1),
+    ap.add_argument("--narrow-codes", type=int, default=0, choices=(0, 1),
                     help="1: symbols / indexes cross to the host rANS coder as int16 / uint8 on a copy stream (overlapping "
                          "the next compress); 0: int32 on the encoder stream")
     ap.add_argument("--per-image", type=int, default=1,
@@ -257,11 +257,11 @@ def main():
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    # (the team schedule decodes on one stream: only that one is created, so the copy stream of compress_side, created
-    # last, gets a hardware queue of its own -- one shared with the team decoder's would wait behind its second-long
-    # launches; the order encoder, decoder(s) is the measured one)
-    n_dec_streams = ndec if not args.team else (2 if args.gang > 1 else 1)
-    s_enc, *s_decs, s_copy = dedicated_streams(2 + n_dec_streams, dev)
+    s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
+    # the copy stream of compress_side (--narrow-codes 1): one of the decoder streams the team schedule leaves idle, on
+    # a hardware queue of its own (a stream sharing the team decoder's queue waits behind its second-long launches;
+    # creating fewer or reordered streams moved the encoder / decoder queues and cost 10 %: profiles/r03_exp)
+    s_copy = s_decs[-2] if args.team and len(s_decs) > 2 else dedicated_streams(1, dev)[0]
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-for nc in 1 0 1 0; do
+for nc in 0 1 0 1; do
   timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --cpu-budget 0 --side-steps 0 --per-image 0 --narrow-codes $nc > $O/r03_bench13_nc${nc}_$RANDOM.log 2>&1 || exit 2
 done
 for f in $O/r03_bench13_nc*.log; do python3 -c "
