@@ -119,9 +119,6 @@ def parse_args(argv=None):
     ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
                     help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
                          "still decoded as its own 32-frame batch)")
-    ap.add_argument("--narrow-codes", type=int, default=0, choices=(0, 1),
-                    help="1: symbols / indexes cross to the host rANS coder as int16 / uint8 on a copy stream (overlapping "
-                         "the next compress); 0: int32 on the encoder stream")
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
@@ -258,10 +255,8 @@ def main():
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
     s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
-    # the copy stream of compress_side (--narrow-codes 1): one of the decoder streams the team schedule leaves idle, on
-    # a hardware queue of its own (a stream sharing the team decoder's queue waits behind its second-long launches;
-    # creating fewer or reordered streams moved the encoder / decoder queues and cost 10 %: profiles/r03_exp)
-    s_copy = s_decs[-2] if args.team and len(s_decs) > 2 else dedicated_streams(1, dev)[0]
+    # (creating only the streams the team schedule uses, or another order, moved the encoder's and the decoder's hardware
+    # queues and cost 10 %: profiles/r03_exp/r03_bench13_*)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
@@ -299,43 +294,18 @@ def main():
     enc_acc = dict(on=False, ms=0.0, passes=0)     # HIP-event time of the encoder graphs in the timed region
 
     def compress_side(ph, xb, model=None, stream=None):
-        """GPU compress on the encoder stream.  The symbols / indexes go to page-locked host buffers for the host rANS
-        coder (the reference's coder is host C++), narrowed on the GPU to int16 / uint8 (indexes are 0..63; a symbol
-        outside int16 -- never at these operating points -- makes entropy_side fetch the int32 tensor instead) and
-        copied on a copy stream, so the transfer overlaps the next batch's compress instead of following it on the
-        encoder stream (`--narrow-codes 0`: int32, on the encoder stream)."""
+        """GPU compress on the encoder stream; symbols/indexes DMA'd into page-locked host buffers there (for the host
+        rANS coder: the reference's coder is host C++).  (Narrowing them to int16 / uint8 and copying on a stream of its
+        own moved 2-8 ms per batch off the encoder stream but gained 0.5 %, within noise: profiles/r03_exp.)"""
         model, stream = model or enc_model, stream or s_enc
         t0 = time.perf_counter()
         with torch.cuda.stream(stream):
             r = model.compress_batch(xb)
-            if args.narrow_codes:
-                sym32 = r["symbols"]
-                dev_codes = (sym32.to(torch.int16), r["indexes"].to(torch.uint8),
-                             (sym32.abs().amax() <= 32767).reshape(1))
-                ev = torch.cuda.Event()
-                ev.record(stream)
-        if args.narrow_codes:
-            with torch.cuda.stream(s_copy):
-                s_copy.wait_event(ev)
-                host = []
-                for d in dev_codes:
-                    h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
-                    h.copy_(d, non_blocking=True)
-                    d.record_stream(s_copy)
-                    host.append(h)
-                done = torch.cuda.Event()
-                done.record(s_copy)
-            sym32.record_stream(s_copy)
-            r["symbols"], r["indexes"] = host[0], host[1]
-            r["_codes"] = (done, host[2], sym32)
-            stream.synchronize()            # the compress itself (its HIP-event timing below); not the copy
-        else:
-            with torch.cuda.stream(stream):
-                for k in ("symbols", "indexes"):
-                    h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
-                    h.copy_(r[k], non_blocking=True)
-                    r[k] = h
-                stream.synchronize()
+            for k in ("symbols", "indexes"):
+                h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
+                h.copy_(r[k], non_blocking=True)
+                r[k] = h
+            stream.synchronize()
         e_ms = model.last_timing()[0] if enc_acc["on"] else 0.0
         with plock:
             ph["encode"] += time.perf_counter() - t0
@@ -346,22 +316,10 @@ def main():
 
     def split_record(r, e):
         """Batch e (n frames) of a multi-batch compress record."""
-        out = {}
-        for kk, v in r.items():
-            if kk == "_codes":
-                out[kk] = (v[0], v[1], v[2][e * n:(e + 1) * n])
-            else:
-                out[kk] = v[e * n:(e + 1) * n] if v is not None else None
-        return out
+        return {kk: (v[e * n:(e + 1) * n] if v is not None else None) for kk, v in r.items()}
 
     def entropy_side(r, fmt, ph, model=None):
         t0 = time.perf_counter()
-        if "_codes" in r:          # narrowed transport (compress_side): wait for its copy, check the int16 range
-            done, fits, sym32 = r.pop("_codes")
-            done.synchronize()
-            if not bool(fits[0]):
-                r["symbols"] = sym32.cpu()
-            del sym32
         st = (model or enc_model).entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
         with plock:
             ph["entropy"] += time.perf_counter() - t0
