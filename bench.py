@@ -254,7 +254,13 @@ def main():
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
     # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    s_enc, *s_decs = dedicated_streams(1 + ndec, dev)
+    # experiment hooks: idle streams created before the encoder's (LBIC_BENCH_STREAM_PRE) and between the encoder's and
+    # the decoders' (LBIC_BENCH_STREAM_GAP) -- they move the hardware queues the busy streams land on
+    pre = dedicated_streams(int(os.environ.get("LBIC_BENCH_STREAM_PRE", "0")), dev)
+    s_enc, = dedicated_streams(1, dev)
+    gap = dedicated_streams(int(os.environ.get("LBIC_BENCH_STREAM_GAP", "0")), dev)
+    s_decs = dedicated_streams(ndec, dev)
+    del pre, gap
     # (creating only the streams the team schedule uses, or another order, moved the encoder's and the decoder's hardware
     # queues and cost 10 %: profiles/r03_exp/r03_bench13_*)
     enc_model = make_model()
