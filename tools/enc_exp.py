@@ -27,6 +27,8 @@ def main():
     m = BlockBasedImgCompLossyNetv9(cfg)
     m.load_state_dict(synth_state_dict(arch, 1337, rate="low"))
     m.update(force=True)
+    if os.environ.get("LDS_FLOOR"):
+        m.set_encoder_lds_floor(int(os.environ["LDS_FLOOR"]))
     fr = np.stack([image_to_blocks(np.random.default_rng(k).integers(0, 256, (3, size, size), dtype=np.uint8)
                                    .astype(np.float32) / 255.0 - 0.5, 8) for k in range(n)])
     x = torch.from_numpy(fr).cuda()
@@ -40,7 +42,7 @@ def main():
     h = hashlib.sha256()
     for k in ("symbols", "indexes", "zhat"):
         h.update(r[k].cpu().numpy().tobytes())
-    print(json.dumps(dict(tiled=os.environ.get("LBIC_ENC_TILED", "default"), cfg=os.environ.get("LBIC_ENC_CFG", "0"), encode_ms=[round(t, 2) for t in ts],
+    print(json.dumps(dict(tiled=os.environ.get("LBIC_ENC_TILED", "default"), cfg=os.environ.get("LBIC_ENC_CFG", "0"), lds_floor=os.environ.get("LDS_FLOOR", "0"), encode_ms=[round(t, 2) for t in ts],
                           digest=h.hexdigest()[:16])), flush=True)
 
 
