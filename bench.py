@@ -119,6 +119,11 @@ def parse_args(argv=None):
     ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
                     help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
                          "still decoded as its own 32-frame batch)")
+    ap.add_argument("--dec-cus", type=int, default=0,
+                    help="team schedule: run the team decode launches on a stream restricted to this many CUs of every XCD "
+                         "(teams of that many workgroups) and the encoder on the other CUs (hipExtStreamCreateWithCUMask, "
+                         "lbic.streams.cu_split_streams); the last launch, after the last encode, uses every CU.  0 = both "
+                         "kernels on every CU")
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
@@ -261,6 +266,10 @@ def main():
     gap = dedicated_streams(int(os.environ.get("LBIC_BENCH_STREAM_GAP", "0")), dev)
     s_decs = dedicated_streams(ndec, dev)
     del pre, gap
+    s_dmask = None
+    if args.dec_cus:
+        from lbic.streams import cu_split_streams
+        s_enc, s_dmask = cu_split_streams(args.dec_cus, dev)
     # (creating only the streams the team schedule uses, or another order, moved the encoder's and the decoder's hardware
     # queues and cost 10 %: profiles/r03_exp/r03_bench13_*)
     enc_model = make_model()
@@ -411,13 +420,17 @@ def main():
                             gi += 1
                             t0_ = time.perf_counter()
                             sts = [f_.result() for (_, _, f_) in pend]
-                            with torch.cuda.stream(s_decs[0]):
-                                # the last launch runs with the encoder finished (two workgroups per CU measured slower:
+                            last = gi == len(sizes)
+                            # with --dec-cus every launch but the last runs on the decoder's CUs (the encoder has the
+                            # others); the last runs with the encoder finished, on every CU
+                            sd_ = s_dmask if s_dmask is not None and not last else s_decs[0]
+                            with torch.cuda.stream(sd_):
+                                # (two workgroups per CU for the last launch measured slower:
                                 # profiles/r02_exp/team_two_per_cu.txt)
-                                last = gi == len(sizes)
                                 zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb,
-                                                      wg_per_cu=args.drain_wg_per_cu if last else 1)
-                                s_decs[0].synchronize()
+                                                      wg_per_cu=args.drain_wg_per_cu if last else 1,
+                                                      team_size=args.dec_cus if sd_ is s_dmask else 0)
+                                sd_.synchronize()
                             with plock:
                                 ph["decode"] += time.perf_counter() - t0_
                             if prof:
@@ -681,6 +694,8 @@ def main():
                    "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
                    "decode_passes_in_flight": args.team or args.workers or depth,
                    "frames_per_encode_pass": n * (args.enc_pass if args.team else 1),
+                   "cu_split": (f"decode launches on {args.dec_cus} CUs of every XCD, the encoder on the others (the "
+                                "last launch on all)" if args.team and args.dec_cus else "none"),
                    "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
                                 f"helper threads; every {args.team} encoded batches are decoded by ONE persistent "
                                 "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "

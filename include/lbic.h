@@ -92,6 +92,10 @@ int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, floa
  * LDS to an encoder running concurrently on another stream.  2: two per CU (teams of 2 * CUs/8), every register
  * of the CU -- for a decode with the GPU otherwise idle (e.g. the last launch of a pipeline).  Results unchanged. */
 #define LBC_OPT_TEAM_WG_PER_CU 2
+/* LBC_OPT_TEAM_SIZE (0..32): workgroups per team of the lbc_decode_team launches this handle leads, one per CU.  0
+ * (default): CUs/8, every CU of an XCD.  Fewer: for a launch on a stream restricted to that many CUs of each XCD
+ * (hipExtStreamCreateWithCUMask; bench.py --dec-cus) while an encoder runs on the remaining CUs.  Results unchanged. */
+#define LBC_OPT_TEAM_SIZE 3
 int lbc_set_option(lbc_model *m, int option, long long value);
 
 /* lbc_encode with flags.  LBC_ENC_FRAME_PAD: the context net's layer-0 map is zero outside the frame

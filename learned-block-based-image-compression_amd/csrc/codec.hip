@@ -181,6 +181,7 @@ struct lbc_model {
     std::vector<int> cell_off, cell_cnt;
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
     int team_wpc = 1;           // LBC_OPT_TEAM_WG_PER_CU
+    int team_size = 0;          // LBC_OPT_TEAM_SIZE (0: CUs / 8)
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -840,6 +841,10 @@ int lbc_set_option(lbc_model* m, int option, long long value) {
         case LBC_OPT_TEAM_WG_PER_CU:
             if (value < 1 || value > 2) return set_error(LBC_E_ARG, "team workgroups per CU must be 1 or 2");
             m->team_wpc = (int)value;
+            return LBC_OK;
+        case LBC_OPT_TEAM_SIZE:
+            if (value < 0 || value > 32) return set_error(LBC_E_ARG, "team size must be 0 (CUs / 8) .. 32");
+            m->team_size = (int)value;
             return LBC_OK;
     }
     return set_error(LBC_E_ARG, "unknown option");
@@ -1547,6 +1552,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
             spread = 1;
         } else {
             S = per_slot;
+            if (m0->team_size > 0) S = std::min(S, m0->team_size * wpc);
             if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
             // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
             // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD

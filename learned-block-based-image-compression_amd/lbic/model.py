@@ -361,12 +361,14 @@ class BlockBasedImgCompLossyNetv9:
 
 
 def decompress_teams(models: Sequence["BlockBasedImgCompLossyNetv9"], batches: Sequence[Sequence[bytes]], Hb: int, Wb: int,
-                     wg_per_cu: int = 1):
+                     wg_per_cu: int = 1, team_size: int = 0):
     """Decode len(batches) <= 8 batches of reference-format bitstreams in ONE persistent launch (lbc_decode_team):
     batch t by models[t] (distinct handles of one geometry, e.g. siblings), each batch the same number of images of
     Hb x Wb blocks.  Returns [zhat_t [n, Hb, Wb, 3B^2]], bit-identical to models[t].decompress_batch(batches[t]).
     wg_per_cu (LBC_OPT_TEAM_WG_PER_CU): 1 leaves room for an encoder running beside the launch; 2 doubles each
-    team's workgroups (every register of the GPU) for a decode with the GPU otherwise idle."""
+    team's workgroups (every register of the GPU) for a decode with the GPU otherwise idle.  team_size
+    (LBC_OPT_TEAM_SIZE): workgroups per team, 0 = one per CU of an XCD; fewer for a launch on a stream restricted to
+    that many CUs per XCD (lbic.streams.cu_split_streams)."""
     T = len(batches)
     if T < 1 or T > 8 or len(models) < T:
         raise ValueError("1 to 8 batches, one model handle each")
@@ -384,5 +386,6 @@ def decompress_teams(models: Sequence["BlockBasedImgCompLossyNetv9"], batches: S
     zp = (ctypes.c_void_p * T)(*[_lib.ptr(z) for z in zh])
     stream = torch.cuda.current_stream(dev).cuda_stream
     _lib.check(_lib.lib().lbc_set_option(models[0]._h, 2, int(wg_per_cu)))
+    _lib.check(_lib.lib().lbc_set_option(models[0]._h, 3, int(team_size)))
     _lib.check(_lib.lib().lbc_decode_team(hs, T, arr, lens, n, Hb, Wb, zp, ctypes.c_void_p(stream)))
     return zh

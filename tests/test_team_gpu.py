@@ -141,6 +141,34 @@ def test_team_small_teams(S, monkeypatch):
         assert torch.equal(got[t], ref[t])
 
 
+@pytest.mark.parametrize("K", [8, 16])
+def test_team_on_cu_masked_stream(K, monkeypatch):
+    """bench.py --dec-cus: a team launch with teams of K workgroups (LBC_OPT_TEAM_SIZE) on a stream restricted to K
+    CUs of every XCD (hipExtStreamCreateWithCUMask), while the encoder codes the next batch on a stream holding the
+    other CUs -- the same results as the graph decoder, and the encoder's results unchanged."""
+    from lbic.model import decompress_teams
+    from lbic.streams import cu_split_streams
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    dev = torch.device("cuda", 0)
+    s_enc, s_dec = cu_split_streams(K, dev)
+    ref, _, hs, st = run_case("b8_lowrate_2rows", 3, 32, 2, 24, seed=K)
+    arch = golden_arch(load_golden("loop_b8_lowrate_2rows"))
+    x = batches(arch, 1, 32, 2, 24, seed=K + 1)[0]
+    want = hs[0].compress_batch(x)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s_enc):
+        enc = hs[0].compress_batch(x)
+    with torch.cuda.stream(s_dec):
+        got = decompress_teams(hs, st, 2, 24, team_size=K)
+        s_dec.synchronize()
+    s_enc.synchronize()
+    for t in range(3):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    for k in ("symbols", "indexes", "zhat"):
+        assert torch.equal(enc[k], want[k])
+    assert hs[0].team_stats()["mode"] == "team_sparse"
+
+
 @pytest.mark.parametrize("name,T,n,shape,scale", [
     ("tiny_ks3111", 3, 5, None, 0.05), ("tiny_ks3311", 8, 3, None, 0.05), ("b8_lowrate_2rows", 4, 32, (2, 24), 0.05),
     ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
