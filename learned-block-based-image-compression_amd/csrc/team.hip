@@ -140,7 +140,13 @@ template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
                                                 float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
-    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments
+#if defined(LBIC_TEAM_DEEP) && LBIC_TEAM_DEEP == 2
+    constexpr bool PF = true, PF2 = true;        // experiment: items j + 1 and j + 2 in flight during item j's chain
+#elif defined(LBIC_TEAM_DEEP)
+    constexpr bool PF = true, PF2 = false;       // experiment: the next item in flight at every slice length
+#else
+    constexpr bool PF = LL <= 7, PF2 = false;    // prefetch the next item's fragments
+#endif
     constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -205,7 +211,21 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         dstamp(dts, 1, 0.f);
         // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
         // hit) so that no load sits behind a branch
-        if constexpr (PF) {
+        if constexpr (PF2) {
+            f4 w2[LL];
+            issue(min(1, ni - 1), w1);
+            for (int j = 0;;) {
+                issue(min(j + 2, ni - 1), w2);
+                chain(j, w0);
+                if (++j >= ni) break;
+                issue(min(j + 2, ni - 1), w0);
+                chain(j, w1);
+                if (++j >= ni) break;
+                issue(min(j + 2, ni - 1), w1);
+                chain(j, w2);
+                if (++j >= ni) break;
+            }
+        } else if constexpr (PF) {
             for (int j = 0;;) {
                 issue(min(j + 1, ni - 1), w1);
                 chain(j, w0);
@@ -368,8 +388,15 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch.
 // DENSE (TeamArgs::dense): the high-rate instance, tables staged in LDS and rans_row<true>; a separate instance so the
 // low-rate one keeps its register allocation.
+#if defined(LBIC_TEAM_DEEP) && LBIC_TEAM_DEEP == 2
+#define LBIC_TEAM_OCC 2
+#elif defined(LBIC_TEAM_DEEP)
+#define LBIC_TEAM_OCC 3
+#else
+#define LBIC_TEAM_OCC 4
+#endif
 template <bool DENSE>
-__global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
+__global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
     // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
     // [dense rANS only: the table image, total16 16-bit entries]
