@@ -1563,7 +1563,13 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         if (S < 1 || (xs && W < 1)) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, xs, W, sparse))) return rc;
         a = m0->team_args;
-        a.dense = sparse ? 0 : 1;   // high rates: the tables staged in every workgroup's LDS (rans_row<true>)
+        // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
+        // far symbols searched in the table image in global memory, or (LBIC_TEAM_SPARSE_LDS=1) in an LDS copy
+        static const bool sparse_lds = [] {
+            const char* e = getenv("LBIC_TEAM_SPARSE_LDS");
+            return e && atoi(e) != 0;
+        }();
+        a.dense = sparse ? (sparse_lds ? 2 : 0) : 1;
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         const int nb = team_blocks_per_cu(a.dense, lds);
@@ -1621,7 +1627,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     }
     m0->team_plain_last = a.plain;
-    m0->team_mode_last = a.dense ? 2 : 1;
+    m0->team_mode_last = a.dense == 1 ? 2 : 1;
     m0->team_xs_last = a.xs;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;

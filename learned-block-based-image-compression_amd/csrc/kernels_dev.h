@@ -607,7 +607,8 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 // SC1: inside k_dec_team (indexes and means from the context net's workgroups by sc1 loads, y_qnt to the decoder's
 // workgroups by sc1 stores, plain ones when wt is false: the whole team shares one L2)
 template <bool SC1 = false>
-__device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true) {
+__device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true,
+                                                const uint16_t* tab = nullptr) {
     RSTAMP(0);
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
@@ -681,7 +682,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         if (t == 0) renorm_slow();
         x = uni64(x);
     };
-    const uint16_t* img16 = a.cdf16;
+    const uint16_t* img16 = tab ? tab : a.cdf16;     // tab: a copy of the table image in LDS (k_dec_team<2>)
     const int lane2 = lane * 2;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {

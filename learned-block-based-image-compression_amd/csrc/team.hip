@@ -395,8 +395,9 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 #else
 #define LBIC_TEAM_OCC 4
 #endif
-template <bool DENSE>
+template <int MODE>
 __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs ta) {
+    constexpr bool DENSE = MODE == 1;
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
     // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
     // [dense rANS only: the table image, total16 16-bit entries]
@@ -441,8 +442,10 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
     const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
     const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
     unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 256 : nullptr;
+    unsigned long long* tsr = ta.ts ? ta.ts + team * 256 : nullptr;   // every rank: [160 + rank] rANS done, [192 + rank]
+                                                                       // the GEMM waves beside it done (sampled step)
     if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
-    if (DENSE) {     // the rANS tables, once per launch (read-only: no hand-off); the census barrier's
+    if (MODE != 0) {     // the rANS tables, once per launch (read-only: no hand-off); the census barrier's
         const uint4* src = reinterpret_cast<const uint4*>(R.cdf16);      // __syncthreads (or the one below) orders them
         uint4* dst = reinterpret_cast<uint4*>(tab);
         for (int i = threadIdx.x; i < R.total16 / 8; i += blockDim.x) dst[i] = src[i];
@@ -480,16 +483,20 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
+                    const bool sstep = tsr && v == ta.sv && h == ta.sh && rank < 32;
                     if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
                         for (int r = rank; r < R.rows; r += S) {
                             if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
+                            else if constexpr (MODE == 2) rans_row_sparse<true>(R, lwin, r, lane, wt, tab);
                             else rans_row_sparse<true>(R, lwin, r, lane, wt);
                         }
+                        if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
                         int nt0, ntn;
                         cols(g, nt0, ntn);
                         team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy);
+                        if (sstep && threadIdx.x == 0) tsr[192 + rank] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
@@ -527,7 +534,9 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
 }
 
 static const void* team_instance(int dense) {
-    return dense ? reinterpret_cast<const void*>(&k_dec_team<true>) : reinterpret_cast<const void*>(&k_dec_team<false>);
+    return dense == 1   ? reinterpret_cast<const void*>(&k_dec_team<1>)
+           : dense == 2 ? reinterpret_cast<const void*>(&k_dec_team<2>)
+                        : reinterpret_cast<const void*>(&k_dec_team<0>);
 }
 
 int team_blocks_per_cu(int dense, size_t lds) {
@@ -539,7 +548,7 @@ int team_blocks_per_cu(int dense, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)a.dense * a.tab16 * 2;
+    return (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
@@ -547,7 +556,7 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
         return set_error(LBC_E_ARG, "bad team decoder arguments");
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
     static const bool attr = [] {
-        for (int d = 0; d < 2; ++d)
+        for (int d = 0; d < 3; ++d)
             (void)hipFuncSetAttribute(team_instance(d), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -559,8 +568,9 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.xs && (a.W < 1 || a.S != 8 * a.W || a.plain || a.spread != 1 || a.pf))
         return set_error(LBC_E_ARG, "bad column-split team geometry");
     const dim3 grid(a.xs ? 8 * a.T * a.W : 8 * a.S / a.spread);
-    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, grid, dim3(512), lds, s, a);
-    else hipLaunchKernelGGL(k_dec_team<false>, grid, dim3(512), lds, s, a);
+    if (a.dense == 1) hipLaunchKernelGGL(k_dec_team<1>, grid, dim3(512), lds, s, a);
+    else if (a.dense == 2) hipLaunchKernelGGL(k_dec_team<2>, grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_team<0>, grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

@@ -74,6 +74,10 @@ def main():
                               bit_exact=ok, launch_ms=span, sampled_step_us=step, op_us_team0=ops[0],
                               op_us_mean=[round(float(np.mean([o[k] for o in ops])), 2) for k in range(12)],
                               work_us_team0=comp[0], sc1=os.environ.get("LBIC_TEAM_SC1", "0"),
+                              rans_done_us=[round((ts[0][160 + k] - ts[0][3]) / 100.0, 2) if ts[0][160 + k] else None
+                                            for k in range(32)],
+                              gemm_beside_rans_done_us=[round((ts[0][192 + k] - ts[0][3]) / 100.0, 2) if ts[0][192 + k]
+                                                        else None for k in range(32)],
                               intra_cycles_team0=[[ts[0][64 + 8 * k + p] - ts[0][64 + 8 * k] if ts[0][64 + 8 * k + p] else 0
                                                    for p in range(1, 8)] for k in range(12)])),
               flush=True)
