@@ -171,6 +171,11 @@ int lbc_team_mode(const lbc_model *m, int *mode);
  * another (same results); and whether the last team launch ran column-split (1: every team spans all 8 XCD slots, each
  * slot computing a fixed 1/8 of every GEMM's columns, LBIC_TEAM_XS=1) or one XCD slot per team (0). */
 int lbc_team_events(const lbc_model *m, int *sc1_reruns, int *timeouts, int *column_split);
+/* layout of the last team launch led by m: row-tile groups (1 = one barrier per team; G > 1: the team's workgroups
+ * split into G groups, one per 16-image row tile, each with its own barrier, LBIC_TEAM_GROUPS=1) and whether the sparse
+ * rANS variant searched its rare far symbols in an LDS copy of the table image (1, LBIC_TEAM_SPARSE_LDS=1) or in
+ * global memory (0).  No reference counterpart: an observability hook of this implementation's decoder. */
+int lbc_team_layout(const lbc_model *m, int *groups, int *sparse_lds_tables);
 
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder

@@ -215,6 +215,8 @@ struct lbc_model {
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
     int team_timeouts = 0;    // team launches that timed out at a barrier and were decoded through lbc_decode instead
     int team_xs_last = 0;     // the last team launch ran column-split (TeamArgs::xs)
+    int team_groups_last = 1; // its row-tile groups (TeamArgs::groups)
+    int team_sparse_lds_last = 0;   // its sparse rANS searched an LDS table copy (TeamArgs::dense == 2)
     int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
@@ -1455,6 +1457,15 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
         const int items = ((d.M + 15) >> 4) * ntn;
         if (team_fast_path(d, gS, ntn)) a.ni_max = std::max(a.ni_max, (items + gS - 1) / gS);
     }
+    // row-tile groups possible: every GEMM has the same row tiles (MT) and S % MT == 0, no column split (the launch
+    // uses them when LBIC_TEAM_GROUPS=1)
+    a.groups = 1;
+    {
+        const int MT = (n_img + 15) >> 4;
+        bool ok = !xs && MT >= 2 && MT <= 30 && S % MT == 0;
+        for (const GemmArgs& d : gem) ok = ok && ((d.M + 15) >> 4) == MT;
+        if (ok) a.groups = MT;
+    }
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
     // before it run beside the rANS decode when every workgroup takes the fast path for it
     a.split_op = -1;
@@ -1565,11 +1576,10 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a = m0->team_args;
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory, or (LBIC_TEAM_SPARSE_LDS=1) in an LDS copy
-        static const bool sparse_lds = [] {
-            const char* e = getenv("LBIC_TEAM_SPARSE_LDS");
-            return e && atoi(e) != 0;
-        }();
-        a.dense = sparse ? (sparse_lds ? 2 : 0) : 1;
+        const char* sle = getenv("LBIC_TEAM_SPARSE_LDS");
+        a.dense = sparse ? (sle && atoi(sle) ? 2 : 0) : 1;
+        const char* gre = getenv("LBIC_TEAM_GROUPS");
+        if (!(gre && atoi(gre))) a.groups = 1;
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         const int nb = team_blocks_per_cu(a.dense, lds);
@@ -1629,6 +1639,8 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     m0->team_plain_last = a.plain;
     m0->team_mode_last = a.dense == 1 ? 2 : 1;
     m0->team_xs_last = a.xs;
+    m0->team_groups_last = a.xs ? 1 : std::max(a.groups, 1);
+    m0->team_sparse_lds_last = a.dense == 2;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
     m0->dec_timed = true;
@@ -1670,6 +1682,13 @@ int lbc_team_events(const lbc_model* m, int* sc1_reruns, int* timeouts, int* col
     *sc1_reruns = m->team_fallbacks;
     *timeouts = m->team_timeouts;
     *column_split = m->team_xs_last;
+    return LBC_OK;
+}
+
+int lbc_team_layout(const lbc_model* m, int* groups, int* sparse_lds_tables) {
+    if (!m || !groups || !sparse_lds_tables) return set_error(LBC_E_ARG, "null argument");
+    *groups = m->team_groups_last;
+    *sparse_lds_tables = m->team_sparse_lds_last;
     return LBC_OK;
 }
 

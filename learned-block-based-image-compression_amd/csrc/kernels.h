@@ -136,6 +136,10 @@ struct TeamArgs {
                              // ranks over two XCDs; hand-offs write-through, plain = 0)
     int align;               // cross-team step alignment (0 off; 1 teams at most one raster step apart; 2 lockstep):
                              // a launch-wide step counter [(TEAM_MAX + 1) * 32] in `sync`
+    int groups;              // row-tile groups (>= 1; LBIC_TEAM_GROUPS=1): with S % MT == 0 in every GEMM, workgroup rank
+                             // r only ever computes row tile r % MT, so the team splits into MT groups (ranks r % MT == g,
+                             // images 16 g .. 16 g + 15, whose rANS rows are decoded inside the group) that share no data:
+                             // each group has its own barrier counter ([2 + g] of the team's line)
     int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)
                              // of EVERY XCD slot (S = 8 W); the workgroups of slot x compute only the column tiles
                              // team_xs_cols(x) of every GEMM, so each XCD's L2 holds 1/8 of the weights, shared by the

@@ -430,7 +430,9 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
         if (ta.xs) team_xs_cols(NT, slot, nt0, ntn);
         else { nt0 = 0; ntn = NT; }
     };
-    unsigned* ctr = ta.sync + team * 32;
+    // row-tile groups: the ranks r % ngr == grp of the team (ngr = ta.groups; 1 = the whole team) share a barrier counter
+    const int ngr = ta.xs ? 1 : max(ta.groups, 1), grp = rank % ngr, gsz = S / ngr;
+    unsigned* ctr = ta.sync + team * 32 + (ngr > 1 ? 2 + grp : 0);
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -485,7 +487,10 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
                     const bool sstep = tsr && v == ta.sv && h == ta.sh && rank < 32;
                     if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
-                        for (int r = rank; r < R.rows; r += S) {
+                        // rows: every image of the batch (ngr = 1), or the images of this group's row tile
+                        const int r0 = ngr > 1 ? 16 * grp + rank / ngr : rank, rs = ngr > 1 ? gsz : S;
+                        const int r1 = ngr > 1 ? min(16 * grp + 16, R.rows) : R.rows;
+                        for (int r = r0; r < r1; r += rs) {
                             if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
                             else if constexpr (MODE == 2) rans_row_sparse<true>(R, lwin, r, lane, wt, tab);
                             else rans_row_sparse<true>(R, lwin, r, lane, wt);
@@ -500,7 +505,7 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
-                target += S;
+                target += gsz;
                 const GemmArgs* nx = nullptr;
                 if (ta.pf) {     // the GEMM after this barrier (the next step's first at the step's end)
                     int nop = op + 1, ncls = cls;

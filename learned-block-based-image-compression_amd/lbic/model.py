@@ -245,7 +245,8 @@ class BlockBasedImgCompLossyNetv9:
         plain, mode, sc1_reruns, timeout_fallbacks, column_split) -- its duration, algorithmic bytes / FLOPs, the
         hand-off store mode it ran in, how the call decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant,
         or "fallback" to lbc_decode per batch), and the handle's event counters (lbc_team_events): write-through
-        reruns, barrier timeouts decoded through the fallback, whether the last launch ran column-split."""
+        reruns, barrier timeouts decoded through the fallback, whether the last launch ran column-split; its layout
+        (lbc_team_layout): row-tile groups and whether the sparse rANS searched an LDS table copy."""
         L = _lib.lib()
         ms, by, fl, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         _lib.check(L.lbc_team_stats(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(fl), ctypes.byref(pl)))
@@ -253,9 +254,11 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(L.lbc_team_mode(self._h, ctypes.byref(mode)))
         rr, to, xs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(L.lbc_team_events(self._h, ctypes.byref(rr), ctypes.byref(to), ctypes.byref(xs)))
+        gr, sl = ctypes.c_int(), ctypes.c_int()
+        _lib.check(L.lbc_team_layout(self._h, ctypes.byref(gr), ctypes.byref(sl)))
         return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value,
                     mode=("fallback", "team_sparse", "team_dense")[mode.value], sc1_reruns=rr.value,
-                    timeout_fallbacks=to.value, column_split=xs.value)
+                    timeout_fallbacks=to.value, column_split=xs.value, groups=gr.value, sparse_lds_tables=sl.value)
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]

@@ -277,3 +277,36 @@ def test_team_step_alignment(xs, align, monkeypatch):
     for t in range(6):
         assert torch.equal(got[t], ref[t])
     assert hs[0].team_stats()["mode"] == "team_sparse"
+
+
+@pytest.mark.parametrize("sparse_lds", [0, 1])
+@pytest.mark.parametrize("name,T,n,shape,groups", [
+    ("b8_lowrate_2rows", 8, 32, (2, 96), 2), ("b8_lowrate_2rows", 3, 64, (2, 20), 4),
+    ("tiny_ks3311", 2, 20, (3, 4), 2), ("b8_lowrate_2rows", 2, 40, (2, 20), 1), ("tiny_ks3111", 1, 4, None, 1),
+])
+def test_team_row_groups(name, T, n, shape, groups, sparse_lds, monkeypatch):
+    """LBIC_TEAM_GROUPS=1: the team split into one barrier group per 16-image row tile (each group decodes the rANS
+    rows of its own images); 40 images (three row tiles) on 64 workgroups and 4 images (one row tile) keep one group.
+    LBIC_TEAM_SPARSE_LDS=1: the sparse rANS searches its far symbols in an LDS copy of the table image.  Same results
+    as the graph decoder."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    monkeypatch.setenv("LBIC_TEAM_GROUPS", "1")
+    monkeypatch.setenv("LBIC_TEAM_SPARSE_LDS", str(sparse_lds))
+    g = load_golden("loop_" + name)
+    Hb, Wb = shape or g["x"].shape[:2]
+    ref, got, hs, _ = run_case(name, T, n, Hb, Wb, seed=T * 11 + n)
+    for t in range(T):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    st = hs[0].team_stats()
+    assert st["mode"] == "team_sparse" and st["groups"] == groups and st["sparse_lds_tables"] == sparse_lds
+
+
+def test_team_row_groups_dense(monkeypatch):
+    """Row-tile groups with the dense rANS variant (tables in LDS) on streams coded at high amplitude."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
+    monkeypatch.setenv("LBIC_TEAM_GROUPS", "1")
+    ref, got, hs, _ = run_case("b8_lowrate_2rows", 2, 32, 2, 24, seed=5, scale=0.5)
+    for t in range(2):
+        assert torch.equal(got[t], ref[t])
+    st = hs[0].team_stats()
+    assert st["mode"] == "team_dense" and st["groups"] == 2
