@@ -140,6 +140,8 @@ struct TeamArgs {
                              // r only ever computes row tile r % MT, so the team splits into MT groups (ranks r % MT == g,
                              // images 16 g .. 16 g + 15, whose rANS rows are decoded inside the group) that share no data:
                              // each group has its own barrier counter ([2 + g] of the team's line)
+    int prio;                // wave issue priority of the team's waves (s_setprio 0-3; LBIC_TEAM_PRIO): the decoder's
+                             // latency chain ahead of the encoder's waves on a shared SIMD
     int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)
                              // of EVERY XCD slot (S = 8 W); the workgroups of slot x compute only the column tiles
                              // team_xs_cols(x) of every GEMM, so each XCD's L2 holds 1/8 of the weights, shared by the

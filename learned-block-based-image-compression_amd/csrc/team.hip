@@ -412,6 +412,9 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
     // spread 2 (at most four teams): team t = the workgroups of slots 2t and 2t + 1 (two XCDs), ranks interleaved
     // xs (column-split): grid = 8 x T W; team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W) of every slot,
     // rank = slot W + q % W; in a GEMM the W workgroups of slot x share the column tiles team_xs_cols(x)
+    if (ta.prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (ta.prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (ta.prio >= 3) __builtin_amdgcn_s_setprio(3);
     const int slot = blockIdx.x & 7;
     int team, rank;
     if (ta.xs) {

@@ -282,11 +282,13 @@ def test_team_step_alignment(xs, align, monkeypatch):
 @pytest.mark.parametrize("sparse_lds", [0, 1])
 @pytest.mark.parametrize("name,T,n,shape,groups", [
     ("b8_lowrate_2rows", 8, 32, (2, 96), 2), ("b8_lowrate_2rows", 3, 64, (2, 20), 4),
-    ("tiny_ks3311", 2, 20, (3, 4), 2), ("b8_lowrate_2rows", 2, 40, (2, 20), 1), ("tiny_ks3111", 1, 4, None, 1),
+    ("tiny_ks3311", 2, 20, (3, 4), 1), ("tiny_ks3111", 2, 20, None, 2), ("b8_lowrate_2rows", 2, 40, (2, 20), 1),
+    ("tiny_ks3111", 1, 4, None, 1),
 ])
 def test_team_row_groups(name, T, n, shape, groups, sparse_lds, monkeypatch):
     """LBIC_TEAM_GROUPS=1: the team split into one barrier group per 16-image row tile (each group decodes the rANS
-    rows of its own images); 40 images (three row tiles) on 64 workgroups and 4 images (one row tile) keep one group.
+    rows of its own images); 40 images (three row tiles) on 64 workgroups, 4 images (one row tile) and KS3311 (the
+    layer-0 cache GEMM has a row per cell, not per image) keep one group.
     LBIC_TEAM_SPARSE_LDS=1: the sparse rANS searches its far symbols in an LDS copy of the table image.  Same results
     as the graph decoder."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
