@@ -1578,6 +1578,8 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // far symbols searched in the table image in global memory, or (LBIC_TEAM_SPARSE_LDS=1) in an LDS copy
         const char* sle = getenv("LBIC_TEAM_SPARSE_LDS");
         a.dense = sparse ? (sle && atoi(sle) ? 2 : 0) : 1;
+        const char* rpe = getenv("LBIC_TEAM_RPERSIST");
+        a.rpersist = rpe ? (atoi(rpe) != 0) : 1;
         const char* pre = getenv("LBIC_TEAM_PRIO");
         a.prio = pre ? std::max(0, std::min(3, atoi(pre))) : 0;
         const char* gre = getenv("LBIC_TEAM_GROUPS");

@@ -140,6 +140,8 @@ struct TeamArgs {
                              // r only ever computes row tile r % MT, so the team splits into MT groups (ranks r % MT == g,
                              // images 16 g .. 16 g + 15, whose rANS rows are decoded inside the group) that share no data:
                              // each group has its own barrier counter ([2 + g] of the team's line)
+    int rpersist;            // 1: a workgroup that decodes one image per step keeps its rANS coder state, window and
+                             // table metadata in LDS between steps (sparse variant; LBIC_TEAM_RPERSIST, default on)
     int prio;                // wave issue priority of the team's waves (s_setprio 0-3; LBIC_TEAM_PRIO): the decoder's
                              // latency chain ahead of the encoder's waves on a shared SIMD
     int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)

@@ -606,9 +606,14 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 // for it -- and each wave is independent.  Bit-identical to rans_row (same coder, same tables).
 // SC1: inside k_dec_team (indexes and means from the context net's workgroups by sc1 loads, y_qnt to the decoder's
 // workgroups by sc1 stores, plain ones when wt is false: the whole team shares one L2)
-template <bool SC1 = false>
+// PERSIST (k_dec_team, a workgroup that decodes the same single image at every raster step): the coder state (x, p),
+// the window base, the stream's word range and the table metadata stay in an LDS cache `lc` ([0..1] x, [2] p, [3] the
+// window's first word, [4] valid, [5..6] word base, [7] word count, [64..575] tmeta) between the raster steps, and the
+// window is refilled from global memory only when fewer words than one block can consume remain in it: the step's
+// only global reads are then the block's scale indexes (written by the context net this step).
+template <bool SC1 = false, bool PERSIST = false>
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true,
-                                                const uint16_t* tab = nullptr) {
+                                                const uint16_t* tab = nullptr, uint32_t* lc = nullptr) {
     RSTAMP(0);
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
@@ -620,22 +625,42 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     }
     img = __builtin_amdgcn_readfirstlane(img);
     const int Mlat = a.Mlat;
-    const int t_fb = a.tmeta[lane], t_S = a.tmeta[64 + lane], t_lm2 = a.tmeta[128 + lane];
-    const int t_ca = a.tmeta[192 + lane], t_off = a.tmeta[256 + lane], t_lf = a.tmeta[320 + lane];
-    const int t_lfm = a.tmeta[384 + lane], t_lfp = a.tmeta[448 + lane];
-    const unsigned long long x_in = a.state_x[img];
-    const int p_in = a.state_ptr[img];
-    const long long wb = a.word_base[img];
-    const int nw_in = a.word_count[img];
     int ti[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) ti[kb] = ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1)) & 63;
-    unsigned long long x = uni64(x_in);
-    int p = __builtin_amdgcn_readfirstlane(p_in);
+    int t_fb, t_S, t_lm2, t_ca, t_off, t_lf, t_lfm, t_lfp;
+    unsigned long long x;
+    int p, nw, p0;
+    long long wb;
+    bool have = false;
+    if constexpr (PERSIST) have = __builtin_amdgcn_readfirstlane((int)lc[4]) == 1;
+    if (have) {
+        t_fb = (int)lc[64 + lane]; t_S = (int)lc[128 + lane]; t_lm2 = (int)lc[192 + lane]; t_ca = (int)lc[256 + lane];
+        t_off = (int)lc[320 + lane]; t_lf = (int)lc[384 + lane]; t_lfm = (int)lc[448 + lane]; t_lfp = (int)lc[512 + lane];
+        x = uni64(((unsigned long long)lc[1] << 32) | lc[0]);
+        p = __builtin_amdgcn_readfirstlane((int)lc[2]);
+        p0 = __builtin_amdgcn_readfirstlane((int)lc[3]);
+        wb = (long long)(((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)lc[6]) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)lc[5]));
+        nw = __builtin_amdgcn_readfirstlane((int)lc[7]);
+    } else {
+        t_fb = a.tmeta[lane]; t_S = a.tmeta[64 + lane]; t_lm2 = a.tmeta[128 + lane];
+        t_ca = a.tmeta[192 + lane]; t_off = a.tmeta[256 + lane]; t_lf = a.tmeta[320 + lane];
+        t_lfm = a.tmeta[384 + lane]; t_lfp = a.tmeta[448 + lane];
+        const unsigned long long x_in = a.state_x[img];
+        const int p_in = a.state_ptr[img];
+        wb = a.word_base[img];
+        const int nw_in = a.word_count[img];
+        x = uni64(x_in);
+        p = __builtin_amdgcn_readfirstlane(p_in);
+        nw = __builtin_amdgcn_readfirstlane(nw_in);
+        p0 = p;
+    }
     const uint32_t* w = a.words + wb;
-    const int nw = __builtin_amdgcn_readfirstlane(nw_in);
-    const int p0 = p;
-    {
+    // (re)fill the window from p: always without the cache, with it once fewer words remain than a block can take
+    // (<= 52 bits per symbol incl. a bypass escape)
+    if (!have || p - p0 > RANS_WIN - (52 * Mlat + 31) / 32 - 2) {
+        p0 = p;
         uint32_t wv[RANS_WIN / 64];
 #pragma unroll
         for (int k = 0; k < RANS_WIN / 64; ++k) wv[k] = w[min(p0 + k * 64 + lane, max(nw - 1, 0))];
@@ -664,9 +689,10 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     if (!valid) return;
     RSTAMP(1);
     int bad = 0;
-    int q0 = 0;
-    uint32_t wbuf = lwin[lane];
-    uint32_t wn = rdlane(wbuf, 0);
+    // the 64-word chunk of the window that holds word p (p0: the window's first word)
+    int q0 = min((p - p0) & ~63, RANS_WIN - 64);
+    uint32_t wbuf = lwin[q0 + lane];
+    uint32_t wn = rdlane(wbuf, min(p - p0 - q0, 63));
     auto renorm_slow = [&]() {           // x < 2^31: shift in the next stream word
         x = (x << 32) | wn;
         ++p;
@@ -790,6 +816,25 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         a.state_x[img] = x;
         a.state_ptr[img] = p;
         if (bad) a.status[img] = bad;
+    }
+    if constexpr (PERSIST) {
+        if (!have) {
+            lc[64 + lane] = (uint32_t)t_fb; lc[128 + lane] = (uint32_t)t_S; lc[192 + lane] = (uint32_t)t_lm2;
+            lc[256 + lane] = (uint32_t)t_ca; lc[320 + lane] = (uint32_t)t_off; lc[384 + lane] = (uint32_t)t_lf;
+            lc[448 + lane] = (uint32_t)t_lfm; lc[512 + lane] = (uint32_t)t_lfp;
+            if (lane == 0) {
+                lc[5] = (uint32_t)wb;
+                lc[6] = (uint32_t)((unsigned long long)wb >> 32);
+                lc[7] = (uint32_t)nw;
+            }
+        }
+        if (lane == 0) {
+            lc[0] = (uint32_t)x;
+            lc[1] = (uint32_t)(x >> 32);
+            lc[2] = (uint32_t)p;
+            lc[3] = (uint32_t)p0;
+            lc[4] = 1u;
+        }
     }
     RSTAMP(3);
 }

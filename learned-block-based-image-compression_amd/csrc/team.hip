@@ -3,6 +3,8 @@
 
 namespace lbic {
 
+constexpr int RC_WORDS = 576;   // rans_row_sparse's persistent coder-state cache (see kernels_dev.h)
+
 // ----------------------------------------------------------------------------------------- team decoder
 // k_dec_team: the reference-format raster decodes of T <= 8 batches in ONE persistent launch.  Team t = the S
 // workgroups with blockIdx % 8 == t decodes batch t (a team's workgroups share one XCD under the observed round-robin
@@ -399,13 +401,16 @@ template <int MODE>
 __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs ta) {
     constexpr bool DENSE = MODE == 1;
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
-    // [rANS window RANS_WIN words][barrier flag, padded to 16 B][8 prefetch sink words][GEMM partials ni_max x KSPLIT x 256 floats]
+    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][barrier flag, padded to 16 B][8 prefetch sink words]
+    // [GEMM partials ni_max x KSPLIT x 256 floats]
     // [dense rANS only: the table image, total16 16-bit entries]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
     uint32_t* lwin = team_lds;
-    int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN);
-    float* sink = reinterpret_cast<float*>(team_lds + RANS_WIN + 4);     // team_prefetch's unread word per wave
-    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + 12);
+    uint32_t* rcache = team_lds + RANS_WIN;                              // rans_row_sparse<.., true>'s state cache
+    int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN + RC_WORDS);
+    float* sink = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 4);     // team_prefetch's unread word per wave
+    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 12);
+    if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
@@ -493,10 +498,16 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                         // rows: every image of the batch (ngr = 1), or the images of this group's row tile
                         const int r0 = ngr > 1 ? 16 * grp + rank / ngr : rank, rs = ngr > 1 ? gsz : S;
                         const int r1 = ngr > 1 ? min(16 * grp + 16, R.rows) : R.rows;
-                        for (int r = r0; r < r1; r += rs) {
-                            if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
-                            else if constexpr (MODE == 2) rans_row_sparse<true>(R, lwin, r, lane, wt, tab);
-                            else rans_row_sparse<true>(R, lwin, r, lane, wt);
+                        if (!DENSE && ta.rpersist && r0 < r1 && r0 + rs >= r1) {
+                            // one image per workgroup, the same one at every step: the coder state stays in LDS
+                            if constexpr (MODE == 2) rans_row_sparse<true, true>(R, lwin, r0, lane, wt, tab, rcache);
+                            else if constexpr (!DENSE) rans_row_sparse<true, true>(R, lwin, r0, lane, wt, nullptr, rcache);
+                        } else {
+                            for (int r = r0; r < r1; r += rs) {
+                                if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
+                                else if constexpr (MODE == 2) rans_row_sparse<true>(R, lwin, r, lane, wt, tab);
+                                else rans_row_sparse<true>(R, lwin, r, lane, wt);
+                            }
                         }
                         if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
@@ -556,7 +567,7 @@ int team_blocks_per_cu(int dense, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
+    return (size_t)(RANS_WIN + RC_WORDS + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
