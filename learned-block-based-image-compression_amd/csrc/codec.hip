@@ -1491,20 +1491,6 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
             a.split_wy = wy;
         }
     }
-    // LDS staging of the split GEMM's last K slice (used when LBIC_TEAM_WPRE=1): one slice after the rANS barrier,
-    // at most 8 items per workgroup (one staging wave each), fast path
-    a.wpre = a.wpre_ll = 0;
-    if (a.split_op >= 0 && a.split_wy == KSPLIT - 1 && !xs) {
-        const GemmArgs& d = gem[(size_t)NG + ops[a.split_op]];
-        const int nkb = d.K >> 4, L = nkb / KSPLIT;
-        const int MT = (d.M + 15) >> 4, items = MT * ((d.N + 15) >> 4);
-        const int ni = (items + S - 1) / S;
-        const int LL = (nkb % KSPLIT) == 0 ? L : L + 1;
-        if (L >= 1 && L <= 7 && ni <= KSPLIT - 1 && !d.square_a) {
-            a.wpre = ni * LL;
-            a.wpre_ll = LL;
-        }
-    }
     // algorithmic work of one raster step (the graph decoder's accounting, gemm(): weights + A rows + outputs [+ the
     // GDN input] once per GEMM; rANS: indexes and means in, y_qnt out, the step's stream words)
     double sb = 0, sf = 0;
@@ -1592,8 +1578,6 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // far symbols searched in the table image in global memory, or (LBIC_TEAM_SPARSE_LDS=1) in an LDS copy
         const char* sle = getenv("LBIC_TEAM_SPARSE_LDS");
         a.dense = sparse ? (sle && atoi(sle) ? 2 : 0) : 1;
-        // the split GEMM's last K slice staged in LDS beside the rANS decode (opt-in, LBIC_TEAM_WPRE=1)
-        if (const char* e = getenv("LBIC_TEAM_WPRE"); !(e && atoi(e))) a.wpre = a.wpre_ll = 0;
         const char* rpe = getenv("LBIC_TEAM_RPERSIST");
         a.rpersist = rpe ? (atoi(rpe) != 0) : 1;
         const char* pre = getenv("LBIC_TEAM_PRIO");

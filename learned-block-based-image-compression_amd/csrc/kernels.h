@@ -140,9 +140,6 @@ struct TeamArgs {
                              // r only ever computes row tile r % MT, so the team splits into MT groups (ranks r % MT == g,
                              // images 16 g .. 16 g + 15, whose rANS rows are decoded inside the group) that share no data:
                              // each group has its own barrier counter ([2 + g] of the team's line)
-    int wpre, wpre_ll;       // > 0 (LBIC_TEAM_WPRE=1, split GEMM with one K slice after the rANS barrier): 1 KB fragment
-                             // blocks of LDS (items x wpre_ll) into which the idle waves stage that slice's weights
-                             // beside the rANS decode; the slice then reads them from LDS
     int rpersist;            // 1: a workgroup that decodes one image per step keeps its rANS coder state, window and
                              // table metadata in LDS between steps (sparse variant; LBIC_TEAM_RPERSIST, default on)
     int prio;                // wave issue priority of the team's waves (s_setprio 0-3; LBIC_TEAM_PRIO): the decoder's

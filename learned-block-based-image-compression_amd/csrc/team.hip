@@ -138,12 +138,9 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 #endif
 }
 
-// WL: the weight fragments come from `wl` in LDS ([item j][c < LL] x 64 lanes, staged beside the rANS decode by the
-// workgroup's idle waves: team_stage_split_w) instead of global memory (the phase-2 tail of the split GEMM)
-template <int L, bool EXACT, bool SQ, bool WL = false>
+template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
-                                                float* red, bool wt, int ph, int wy, unsigned long long* dts,
-                                                const f4* wl = nullptr) {
+                                                float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
 #if defined(LBIC_TEAM_DEEP) && LBIC_TEAM_DEEP == 2
     constexpr bool PF = true, PF2 = true;        // experiment: items j + 1 and j + 2 in flight during item j's chain
@@ -181,14 +178,9 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
-            if constexpr (WL) {
+            const int nt = nt0 + (rank + j * S) / MT;
 #pragma unroll
-                for (int c = 0; c < LL; ++c) w[c] = wl[(j * LL + c) * 64 + lane];
-            } else {
-                const int nt = nt0 + (rank + j * S) / MT;
-#pragma unroll
-                for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-            }
+            for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
         };
         auto chain = [&](int j, f4 (&w)[LL]) {
             __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
@@ -274,7 +266,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 // [nt0, nt0 + ntn) (the whole GEMM, or -- column-split teams -- the range of this workgroup's XCD slot)
 __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn,
                                               float* red, bool wt, int ph = 0, int wy = 0,
-                                              unsigned long long* dts = nullptr, const f4* wl = nullptr) {
+                                              unsigned long long* dts = nullptr) {
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
     const bool exact = (nkb % KSPLIT) == 0;
@@ -282,21 +274,6 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     const int ni = rank < items ? (items - rank + S - 1) / S : 0;
     if (ni == 0) return;
     if (team_fast_path(g, S, ntn)) {
-#ifdef LBIC_TEAM_WPRE_BUILD   // (an experiment build, liblbic_wpre.so: its extra instances change the kernel's register
-                              // allocation, so the shipped build leaves them out and ignores LBIC_TEAM_WPRE)
-        if (wl && ph == 2 && !g.square_a) {     // the split GEMM's tail on LDS-staged weights
-            switch (L * 2 + (exact ? 1 : 0)) {
-#define LBIC_W(L_)                                                                                          \
-    case L_ * 2 + 1: team_gemm_items<L_, true, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wl); return; \
-    case L_ * 2: team_gemm_items<L_, false, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, wl); return;
-                LBIC_W(1) LBIC_W(2) LBIC_W(3) LBIC_W(4) LBIC_W(5) LBIC_W(6) LBIC_W(7)
-#undef LBIC_W
-                default: break;
-            }
-        }
-#else
-        (void)wl;
-#endif
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                          \
     case L_ * 2 + 1:                                                                                        \
@@ -314,27 +291,6 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     }
     if (ph == 1) return;     // (the host splits a GEMM only where every workgroup takes the path above)
     team_gemm_long(g, v, h, rank, S, nt0, ntn, red, wt);
-}
-
-// Beside the rANS decode: the weight fragments of the split GEMM's last K slice (the one that reads y_qnt, computed after
-// the rANS barrier) for this workgroup's items, staged in LDS by the waves whose own slices are done: wave j < ni stages
-// item j's LL fragments ([j][c] x 64 lanes, the same clamped k-blocks team_gemm_items would load)
-__device__ __forceinline__ void team_stage_split_w(const GemmArgs& g, int rank, int S, int nt0, int ntn, int LL, f4* wl) {
-    const int lane = threadIdx.x & 63;
-    const int j = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nkb = g.K >> 4;
-    const int kb0 = (KSPLIT - 1) * nkb / KSPLIT;
-    const int MT = (g.M + 15) >> 4, items = MT * ntn;
-    const int ni = rank < items ? (items - rank + S - 1) / S : 0;
-    if (j >= ni) return;
-    const int nt = nt0 + (rank + j * S) / MT;
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-    for (int c = 0; c < LL; c += 2) {      // two fragments at a time (few registers: this is off the critical path)
-        const f4 w0 = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-        const f4 w1 = Wt[((long)min(kb0 + c + 1, nkb - 1) * g.NB16 + nt) * 64];
-        wl[(j * LL + c) * 64 + lane] = w0;
-        if (c + 1 < LL) wl[(j * LL + c + 1) * 64 + lane] = w1;
-    }
 }
 
 // The weight fragments of the first NIT items this workgroup computes in GEMM g (each wave: its K slice), requested
@@ -454,7 +410,6 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
     int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN + RC_WORDS);
     float* sink = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 4);     // team_prefetch's unread word per wave
     float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 12);
-    f4* wpre = ta.wpre ? reinterpret_cast<f4*>(red + ta.ni_max * KSPLIT * 256) : nullptr;   // split GEMM's staged weights
     if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
@@ -489,7 +444,7 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint16_t* tab = reinterpret_cast<uint16_t*>(red + ta.ni_max * KSPLIT * 256 + ta.wpre * 256);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(red + ta.ni_max * KSPLIT * 256);
     // the recorded operations are read-only for the launch: constant address space, so their fields come in by
     // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
     typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
@@ -534,7 +489,7 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                     int nt0, ntn;
                     cols(g, nt0, ntn);
                     team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
-                                  samp ? ts + 64 + op * 8 : nullptr, op == ta.split_op ? wpre : nullptr);
+                                  samp ? ts + 64 + op * 8 : nullptr);
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
@@ -560,9 +515,6 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                         int nt0, ntn;
                         cols(g, nt0, ntn);
                         team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy);
-#ifdef LBIC_TEAM_WPRE_BUILD
-                        if (wpre) team_stage_split_w(g, grk, gS, nt0, ntn, ta.wpre_ll, wpre);
-#endif
                         if (sstep && threadIdx.x == 0) tsr[192 + rank] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
@@ -615,8 +567,7 @@ int team_blocks_per_cu(int dense, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + RC_WORDS + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)a.wpre * 1024 +
-           (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
+    return (size_t)(RANS_WIN + RC_WORDS + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
