@@ -112,18 +112,9 @@ def parse_args(argv=None):
                          "the same-command rocprof summary holds only the headline's kernel shapes)")
     ap.add_argument("--substream-steps", type=int, default=0, help="batches in the opt-in sub-stream format (0 = skip)")
     ap.add_argument("--encode-only", type=int, default=0, help="profiling aid: this many encoder passes, no JSON")
-    ap.add_argument("--team-xs", type=int, default=-1, choices=(-1, 0, 1),
-                    help="team decoder geometry: 1 column-split teams (each team spans the 8 XCD slots, each slot a fixed "
-                         "eighth of every GEMM's columns: the decoder weights stay L2-resident), 0 one XCD slot per team, "
-                         "-1 the library default (LBIC_TEAM_XS)")
     ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
                     help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
                          "still decoded as its own 32-frame batch)")
-    ap.add_argument("--dec-cus", type=int, default=0,
-                    help="team schedule: run the team decode launches on a stream restricted to this many CUs of every XCD "
-                         "(teams of that many workgroups) and the encoder on the other CUs (hipExtStreamCreateWithCUMask, "
-                         "lbic.streams.cu_split_streams); the last launch, after the last encode, uses every CU.  0 = both "
-                         "kernels on every CU")
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
@@ -215,8 +206,6 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     dist = world > 1
-    if args.team_xs >= 0:
-        os.environ["LBIC_TEAM_XS"] = str(args.team_xs)
     # test hooks (tests/test_bench_dist_gpu.py runs the N-rank path on a one-GPU box): every rank on one device, and the
     # gloo backend (RCCL refuses two ranks on one GPU).  The driver's runs set neither: one GPU per rank, RCCL.
     local = int(os.environ.get("LBIC_BENCH_DEVICE", local))
@@ -258,20 +247,11 @@ def main():
 
     depth = max(args.depth, 0)
     ndec = max(depth, 2 if args.gang else 1, args.workers - 1, args.team, 1)
-    # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own
-    # experiment hooks: idle streams created before the encoder's (LBIC_BENCH_STREAM_PRE) and between the encoder's and
-    # the decoders' (LBIC_BENCH_STREAM_GAP) -- they move the hardware queues the busy streams land on
-    pre = dedicated_streams(int(os.environ.get("LBIC_BENCH_STREAM_PRE", "0")), dev)
+    # the encoder's and every decoder's stream first, back to back, so each gets a hardware queue of its own (idle
+    # streams created before or between them, only the streams the team schedule uses, or another order moved the
+    # encoder's and the decoder's hardware queues and cost up to 10 %: profiles/r03_exp/r03_q_*, r03_bench13_*)
     s_enc, = dedicated_streams(1, dev)
-    gap = dedicated_streams(int(os.environ.get("LBIC_BENCH_STREAM_GAP", "0")), dev)
     s_decs = dedicated_streams(ndec, dev)
-    del pre, gap
-    s_dmask = None
-    if args.dec_cus:
-        from lbic.streams import cu_split_streams
-        s_enc, s_dmask = cu_split_streams(args.dec_cus, dev)
-    # (creating only the streams the team schedule uses, or another order, moved the encoder's and the decoder's hardware
-    # queues and cost 10 %: profiles/r03_exp/r03_bench13_*)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
     dec_models = [enc_model.sibling() if args.share_weights else make_model() for _ in range(ndec)]
@@ -359,7 +339,7 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, column_split=[])
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0)
 
     def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
@@ -396,7 +376,7 @@ def main():
             dq = queue.Queue(maxsize=2 * team)
             if prof:
                 for kk in team_acc:
-                    team_acc[kk] = [] if kk in ("plain", "column_split") else 0
+                    team_acc[kk] = [] if kk == "plain" else 0
                 team_acc["hw"] = Hb * Wb
                 to0 = dec_models[0].team_stats()["timeout_fallbacks"]
             errs = []
@@ -421,15 +401,12 @@ def main():
                             t0_ = time.perf_counter()
                             sts = [f_.result() for (_, _, f_) in pend]
                             last = gi == len(sizes)
-                            # with --dec-cus every launch but the last runs on the decoder's CUs (the encoder has the
-                            # others); the last runs with the encoder finished, on every CU
-                            sd_ = s_dmask if s_dmask is not None and not last else s_decs[0]
+                            sd_ = s_decs[0]
                             with torch.cuda.stream(sd_):
                                 # (two workgroups per CU for the last launch measured slower:
                                 # profiles/r02_exp/team_two_per_cu.txt)
                                 zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb,
-                                                      wg_per_cu=args.drain_wg_per_cu if last else 1,
-                                                      team_size=args.dec_cus if sd_ is s_dmask else 0)
+                                                      wg_per_cu=args.drain_wg_per_cu if last else 1)
                                 sd_.synchronize()
                             with plock:
                                 ph["decode"] += time.perf_counter() - t0_
@@ -441,7 +418,6 @@ def main():
                                 team_acc["flops"] += st_["flops"]
                                 team_acc["steps"] += len(pend) * Hb * Wb
                                 team_acc["plain"].append(st_["plain"])
-                                team_acc["column_split"].append(st_["column_split"])
                                 team_acc["timeouts"] = st_["timeout_fallbacks"] - to0
                             for (k_, r_, _), st_, z_ in zip(pend, sts, zs):
                                 finish(k_, r_, st_, z_)
@@ -694,8 +670,6 @@ def main():
                    "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
                    "decode_passes_in_flight": args.team or args.workers or depth,
                    "frames_per_encode_pass": n * (args.enc_pass if args.team else 1),
-                   "cu_split": (f"decode launches on {args.dec_cus} CUs of every XCD, the encoder on the others (the "
-                                "last launch on all)" if args.team and args.dec_cus else "none"),
                    "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
                                 f"helper threads; every {args.team} encoded batches are decoded by ONE persistent "
                                 "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "
@@ -777,7 +751,7 @@ def roofline(kstats, dt, team=None, enc=None):
         kernels["k_dec_team"] = dict(launches_sampled=team["launches"], launches_total=team["launches"],
                                      avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
                                      est_share_of_step=round(team["ms"] / 1e3 / dt, 4),
-                                     plain_handoffs=team["plain"], column_split=team["column_split"],
+                                     plain_handoffs=team["plain"],
                                      barrier_timeout_fallbacks=team["timeouts"],
                                      batches_per_launch=round(team["steps"] / team["launches"] / team["hw"], 3),
                                      batch_decode_latency_ms=round(per, 3),

@@ -93,8 +93,8 @@ int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, floa
  * of the CU -- for a decode with the GPU otherwise idle (e.g. the last launch of a pipeline).  Results unchanged. */
 #define LBC_OPT_TEAM_WG_PER_CU 2
 /* LBC_OPT_TEAM_SIZE (0..32): workgroups per team of the lbc_decode_team launches this handle leads, one per CU.  0
- * (default): CUs/8, every CU of an XCD.  Fewer: for a launch on a stream restricted to that many CUs of each XCD
- * (hipExtStreamCreateWithCUMask; bench.py --dec-cus) while an encoder runs on the remaining CUs.  Results unchanged. */
+ * (default): CUs/8, every CU of an XCD.  Fewer: small teams (every workgroup then computes more output tiles and
+ * decodes several rANS streams per step).  Results unchanged. */
 #define LBC_OPT_TEAM_SIZE 3
 int lbc_set_option(lbc_model *m, int option, long long value);
 
@@ -166,16 +166,10 @@ int lbc_team_stats(const lbc_model *m, double *launch_ms, double *bytes, double 
  * sparse rANS variant, 2 one team launch with the dense variant (tables in LDS). */
 int lbc_team_mode(const lbc_model *m, int *mode);
 /* counters of the lbc_decode_team calls led by m: launches rerun with write-through hand-offs after the placement
- * census found a team spread over XCDs; launches in which a workgroup timed out at a team barrier (the grid was not
- * co-resident in time, e.g. CUs held by another process) and whose batches were then decoded by lbc_decode one after
- * another (same results); and whether the last team launch ran column-split (1: every team spans all 8 XCD slots, each
- * slot computing a fixed 1/8 of every GEMM's columns, LBIC_TEAM_XS=1) or one XCD slot per team (0). */
-int lbc_team_events(const lbc_model *m, int *sc1_reruns, int *timeouts, int *column_split);
-/* layout of the last team launch led by m: row-tile groups (1 = one barrier per team; G > 1: the team's workgroups
- * split into G groups, one per 16-image row tile, each with its own barrier, LBIC_TEAM_GROUPS=1) and whether the sparse
- * rANS variant searched its rare far symbols in an LDS copy of the table image (1, LBIC_TEAM_SPARSE_LDS=1) or in
- * global memory (0).  No reference counterpart: an observability hook of this implementation's decoder. */
-int lbc_team_layout(const lbc_model *m, int *groups, int *sparse_lds_tables);
+ * census found a team spread over XCDs; and launches in which a workgroup timed out at a team barrier (the grid was
+ * not co-resident in time, e.g. CUs held by another process) and whose batches were then decoded by lbc_decode one
+ * after another (same results).  Any other launch failure is returned as LBC_E_STATE. */
+int lbc_team_events(const lbc_model *m, int *sc1_reruns, int *timeouts);
 
 /* OPT-IN sub-stream format (not the reference's bitstream): one rANS stream per block row,
  * container [u32 'LBW1'][u32 Hb][u32 bytes[Hb]][row streams...], each row stream in the same coder

@@ -214,9 +214,6 @@ struct lbc_model {
     std::vector<unsigned long long> team_ts_host;
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
     int team_timeouts = 0;    // team launches that timed out at a barrier and were decoded through lbc_decode instead
-    int team_xs_last = 0;     // the last team launch ran column-split (TeamArgs::xs)
-    int team_groups_last = 1; // its row-tile groups (TeamArgs::groups)
-    int team_sparse_lds_last = 0;   // its sparse rANS searched an LDS table copy (TeamArgs::dense == 2)
     int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
@@ -1368,13 +1365,12 @@ static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* stre
 }
 
 // The team program (held by ms[0]): every team's raster step recorded from the same run_ctx / run_dec calls that build
-// the graph decoder, for the geometry (S, spread, xs, W); rebuilt when the geometry, any team's buffers or any team's
+// the graph decoder, for the geometry (S, spread); rebuilt when the geometry, any team's buffers or any team's
 // weight set (Net::gen) changed.  Sets ms[0]->team_args (without the per-launch fields) and the step's algorithmic work.
-static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, int S, int spread, int xs, int W,
-                       int sparse) {
+static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, int S, int spread, int sparse) {
     lbc_model* m0 = ms[0];
     int rc;
-    std::vector<long long> key = {T, S, spread, xs, W, n_img, Hb, Wb, sparse};
+    std::vector<long long> key = {T, S, spread, n_img, Hb, Wb, sparse};
     for (int t = 0; t < T; ++t) {
         lbc_model* m = ms[t];
         for (long long x : {(long long)m->words.p, (long long)m->zpad.p, (long long)m->lane[0].ctx0.p,
@@ -1437,48 +1433,26 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     a.T = T;
     a.S = S;
     a.spread = spread;
-    a.xs = xs;
-    a.W = W;
     a.Hb = Hb;
     a.Wb = Wb;
     a.sync = m0->team_sync.as<unsigned>();
-    // a GEMM's tile share: S workgroups over all column tiles, or (xs) W workgroups over the widest slot's columns
-    auto share = [&](const GemmArgs& d, int& gS, int& ntn) {
-        const int NT = (d.N + 15) >> 4;
-        gS = xs ? W : S;
-        ntn = xs ? (NT + TEAM_MAX - 1) / TEAM_MAX : NT;
-    };
     // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
     a.ni_max = 2;
     a.tab16 = rans[0].total16;
     for (const GemmArgs& d : gem) {
-        int gS, ntn;
-        share(d, gS, ntn);
-        const int items = ((d.M + 15) >> 4) * ntn;
-        if (team_fast_path(d, gS, ntn)) a.ni_max = std::max(a.ni_max, (items + gS - 1) / gS);
-    }
-    // row-tile groups possible: every GEMM has the same row tiles (MT) and S % MT == 0, no column split (the launch
-    // uses them when LBIC_TEAM_GROUPS=1)
-    a.groups = 1;
-    {
-        const int MT = (n_img + 15) >> 4;
-        bool ok = !xs && MT >= 2 && MT <= 30 && S % MT == 0;
-        for (const GemmArgs& d : gem) ok = ok && ((d.M + 15) >> 4) == MT;
-        if (ok) a.groups = MT;
+        const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
+        if (team_fast_path(d, S)) a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
     }
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
     // before it run beside the rANS decode when every workgroup takes the fast path for it
     a.split_op = -1;
     a.split_wy = 0;
     for (int i = 0; i + 1 < (int)ops.size(); ++i) {
-        if (ops[i] != -1 || ops[i + 1] < 0 || getenv("LBIC_TEAM_NOSPLIT")) continue;
+        if (ops[i] != -1 || ops[i + 1] < 0) continue;
         bool fast = true;
         for (int t = 0; t < T; ++t)
             for (int c = 0; c < 3; ++c) {
-                const GemmArgs& d = gem[((size_t)t * 3 + c) * NG + ops[i + 1]];
-                int gS, ntn;
-                share(d, gS, ntn);
-                fast = fast && team_fast_path(d, gS, ntn);
+                fast = fast && team_fast_path(gem[((size_t)t * 3 + c) * NG + ops[i + 1]], S);
             }
         const GemmArgs& d = gem[ops[i + 1]];
         const Seg& last = d.seg[d.nseg - 1];
@@ -1545,45 +1519,27 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[(size_t)t * n_img + i], lens[(size_t)t * n_img + i]);
         if ((rc = upload_streams(m, subs, s))) return rc;
     }
-    // team geometry.  Default (xs = 0): grid 8 x S, one XCD slot per team, S = one (or, LBC_OPT_TEAM_WG_PER_CU, two)
-    // workgroups per CU of an XCD.  Column-split (xs = 1, LBIC_TEAM_XS): every team has W workgroups on each of the 8
-    // slots, W = (workgroups per slot) / T, and the slots split every GEMM's columns.  The whole grid must be resident
-    // (team barriers): the occupancy query below uses the kernel instance and the dynamic LDS of the launch, and a
-    // geometry that does not fit is shrunk (two workgroups per CU -> one) or decoded by lbc_decode per batch.
-    const char* xse = getenv("LBIC_TEAM_XS");
-    const int xs = xse ? (atoi(xse) != 0) : 0;
+    // team geometry: grid 8 x S, one XCD slot per team, S = one (or, LBC_OPT_TEAM_WG_PER_CU, two) workgroups per CU
+    // of an XCD.  The whole grid must be resident (team barriers): the occupancy query below uses the kernel instance
+    // and the dynamic LDS of the launch, and a geometry that does not fit is shrunk (two workgroups per CU -> one) or
+    // decoded by lbc_decode per batch.
     int wpc = std::max(1, m0->team_wpc);
-    int S = 0, spread = 1, W = 0;
+    int S = 0, spread = 1;
     TeamArgs a{};
     for (;;) {
-        const int per_slot = std::min(32, cus / TEAM_MAX) * wpc;
-        if (xs) {
-            W = per_slot / T;
-            S = 8 * W;
-            spread = 1;
-        } else {
-            S = per_slot;
-            if (m0->team_size > 0) S = std::min(S, m0->team_size * wpc);
-            if (const char* e = getenv("LBIC_TEAM_S")) S = std::max(1, std::min(S, atoi(e)));
-            // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
-            // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD
-            const char* spe = getenv("LBIC_TEAM_SPREAD");
-            spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
-            S *= spread;
-        }
-        if (S < 1 || (xs && W < 1)) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
-        if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, xs, W, sparse))) return rc;
+        S = std::min(32, cus / TEAM_MAX) * wpc;
+        if (m0->team_size > 0) S = std::min(S, m0->team_size * wpc);
+        // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
+        // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD
+        const char* spe = getenv("LBIC_TEAM_SPREAD");
+        spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
+        S *= spread;
+        if (S < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+        if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse))) return rc;
         a = m0->team_args;
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
-        // far symbols searched in the table image in global memory, or (LBIC_TEAM_SPARSE_LDS=1) in an LDS copy
-        const char* sle = getenv("LBIC_TEAM_SPARSE_LDS");
-        a.dense = sparse ? (sle && atoi(sle) ? 2 : 0) : 1;
-        const char* rpe = getenv("LBIC_TEAM_RPERSIST");
-        a.rpersist = rpe ? (atoi(rpe) != 0) : 1;
-        const char* pre = getenv("LBIC_TEAM_PRIO");
-        a.prio = pre ? std::max(0, std::min(3, atoi(pre))) : 0;
-        const char* gre = getenv("LBIC_TEAM_GROUPS");
-        if (!(gre && atoi(gre))) a.groups = 1;
+        // far symbols searched in the table image in global memory
+        a.dense = sparse ? 0 : 1;
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         const int nb = team_blocks_per_cu(a.dense, lds);
@@ -1595,10 +1551,6 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     a.tmo = tmoe ? std::max(1ull, strtoull(tmoe, nullptr, 10)) : 100000000ull;
     const char* st = getenv("LBIC_TEAM_STAMPS");
     a.ts = st && atoi(st) ? m0->team_ts.as<unsigned long long>() : nullptr;
-    const char* ale = getenv("LBIC_TEAM_ALIGN");   // cross-team step alignment (0 off, 1 one step of lag, 2 lockstep)
-    a.align = ale ? std::max(0, std::min(2, atoi(ale))) : 0;
-    const char* pfe = getenv("LBIC_TEAM_PF");   // weight tiles of the next GEMM requested at each barrier (0..2)
-    a.pf = pfe && !xs ? std::max(0, std::min(2, atoi(pfe))) : 0;
     a.sv = Hb / 2;
     a.sh = Wb / 2;
     auto reset = [&]() -> int {
@@ -1616,7 +1568,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     // spread over XCDs stops before its first operation (failure word 2, nothing decoded yet) and is rerun with
     // write-through hand-offs
     const char* sc1e = getenv("LBIC_TEAM_SC1");
-    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 || a.xs ? 0 : 1;
+    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 ? 0 : 1;
     unsigned fail = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if ((rc = reset())) return rc;
@@ -1631,20 +1583,21 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         a.plain = 0;
         m0->team_fallbacks += 1;
     }
-    if (fail) {
+    if (fail == 1) {
         // a workgroup gave up waiting at a team barrier (the grid was not co-resident in time: another process or
         // stream held CUs past the timeout).  Nothing is wrong with the streams: decode the batches again through
         // lbc_decode one after another (it re-uploads the streams and resets the workspaces), and count the event.
         m0->team_timeouts += 1;
-        if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
-            fprintf(stderr, "[lbic] team decode: barrier timeout (fail=%u), decoding through lbc_decode\n", fail);
+        static std::atomic<bool> noted{false};
+        const char* ev = getenv("LBIC_TEAM_VERBOSE");
+        if (!noted.exchange(true) || (ev && atoi(ev)))
+            fprintf(stderr, "[lbic] team decode: barrier timeout, decoding through lbc_decode (counted: lbc_team_events)\n");
         return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
     }
+    if (fail)   // any other failure word is a protocol error, not a residency problem: report it
+        return set_error(LBC_E_STATE, "team decode: unexpected failure word " + std::to_string(fail));
     m0->team_plain_last = a.plain;
     m0->team_mode_last = a.dense == 1 ? 2 : 1;
-    m0->team_xs_last = a.xs;
-    m0->team_groups_last = a.xs ? 1 : std::max(a.groups, 1);
-    m0->team_sparse_lds_last = a.dense == 2;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
     m0->dec_timed = true;
@@ -1657,8 +1610,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     }
     HIPCHK(hipStreamSynchronize(s));
     if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
-        fprintf(stderr, "[lbic] team decode: T=%d S=%d xs=%d W=%d plain=%d reruns=%d\n", T, S, a.xs, a.W, a.plain,
-                m0->team_fallbacks);
+        fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d\n", T, S, a.plain, m0->team_fallbacks);
     for (int t = 0; t < T; ++t)
         if ((rc = check_status(ms[t], (size_t)n_img, s))) return rc;
     return LBC_OK;
@@ -1681,18 +1633,10 @@ int lbc_team_mode(const lbc_model* m, int* mode) {
     return LBC_OK;
 }
 
-int lbc_team_events(const lbc_model* m, int* sc1_reruns, int* timeouts, int* column_split) {
-    if (!m || !sc1_reruns || !timeouts || !column_split) return set_error(LBC_E_ARG, "null argument");
+int lbc_team_events(const lbc_model* m, int* sc1_reruns, int* timeouts) {
+    if (!m || !sc1_reruns || !timeouts) return set_error(LBC_E_ARG, "null argument");
     *sc1_reruns = m->team_fallbacks;
     *timeouts = m->team_timeouts;
-    *column_split = m->team_xs_last;
-    return LBC_OK;
-}
-
-int lbc_team_layout(const lbc_model* m, int* groups, int* sparse_lds_tables) {
-    if (!m || !groups || !sparse_lds_tables) return set_error(LBC_E_ARG, "null argument");
-    *groups = m->team_groups_last;
-    *sparse_lds_tables = m->team_sparse_lds_last;
     return LBC_OK;
 }
 

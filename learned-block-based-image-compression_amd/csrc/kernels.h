@@ -49,7 +49,7 @@ struct GemmArgs {
     const int4* blocks;      // per block (img, v, h, 0); row r belongs to block r / P
     const int* ctr;          // optional device counter: blocks += *ctr * ctr_stride (graph replays per row)
     int ctr_stride;
-    int swz;                 // k_gemm: XCD-aware tile order (set by the launcher)
+    int reserved0;           // (unused; keeps the argument block's layout)
     int raster;              // decoder raster step (needs ctr): the block of row r is (raster_img0 + r / P,
     int raster_img0, raster_h;   // *ctr, raster_h), computed instead of loaded from `blocks`
     unsigned long long* ts;  // optional timing slot {max(~start), max(end)} in s_memrealtime ticks (100 MHz)
@@ -116,8 +116,7 @@ struct TeamArgs {
     int nops, NG, T, S, Hb, Wb;
     unsigned* sync;          // [T][32]: per team [0] arrival counter, [1] XCD census (one 128-byte line each), then
                              // [T * 32] the failure word (1 timeout, 2 a team spans XCDs) and [T * 32 + 1] the
-                             // census barrier, [(TEAM_MAX + 1) * 32] the alignment step counter; zeroed before every
-                             // launch
+                             // census barrier; zeroed before every launch
     int plain;               // 1: plain hand-off stores (needs every team on one XCD: checked in-kernel)
     int ni_max;              // most output tiles one workgroup computes in one GEMM of the step (LDS for partials)
     int split_op, split_wy;  // split_op >= 0: the GEMM after the rANS decode; its K slices w < split_wy (no y_qnt)
@@ -126,42 +125,19 @@ struct TeamArgs {
     unsigned long long* ts;  // optional [T][256]: s_memrealtime after every barrier of raster step (sv, sh), then
                              // [64 + 8 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
     int sv, sh;
-    int pf;                  // weight tiles of the NEXT operation each workgroup requests while it waits at a team
-                             // barrier (0 = none): they arrive in the team's L2 before the operation starts
     int dense;               // 1: the streams average >= 1 bit per symbol (high rates): every workgroup stages the
                              // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>
                              // on them; 0: rans_row_sparse (centre intervals, tables from global memory)
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
                              // ranks over two XCDs; hand-offs write-through, plain = 0)
-    int align;               // cross-team step alignment (0 off; 1 teams at most one raster step apart; 2 lockstep):
-                             // a launch-wide step counter [(TEAM_MAX + 1) * 32] in `sync`
-    int groups;              // row-tile groups (>= 1; LBIC_TEAM_GROUPS=1): with S % MT == 0 in every GEMM, workgroup rank
-                             // r only ever computes row tile r % MT, so the team splits into MT groups (ranks r % MT == g,
-                             // images 16 g .. 16 g + 15, whose rANS rows are decoded inside the group) that share no data:
-                             // each group has its own barrier counter ([2 + g] of the team's line)
-    int rpersist;            // 1: a workgroup that decodes one image per step keeps its rANS coder state, window and
-                             // table metadata in LDS between steps (sparse variant; LBIC_TEAM_RPERSIST, default on)
-    int prio;                // wave issue priority of the team's waves (s_setprio 0-3; LBIC_TEAM_PRIO): the decoder's
-                             // latency chain ahead of the encoder's waves on a shared SIMD
-    int xs, W;               // xs = 1, column-split teams: team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W)
-                             // of EVERY XCD slot (S = 8 W); the workgroups of slot x compute only the column tiles
-                             // team_xs_cols(x) of every GEMM, so each XCD's L2 holds 1/8 of the weights, shared by the
-                             // workgroups of all teams on it; hand-offs write-through (plain = 0)
 };
-// the team kernel's fast GEMM path (team_gemm_items) covers g for S workgroups sharing ntn column tiles (ntn < 0: all
-// of g's column tiles): what a split GEMM needs
-__host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S, int ntn = -1) {
+// the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
+__host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
     const int nkb = g.K >> 4, L = nkb / KSPLIT, MT = (g.M + 15) >> 4;
-    const int items = MT * (ntn < 0 ? (g.N + 15) >> 4 : ntn);
+    const int items = MT * ((g.N + 15) >> 4);
     const int ni = (items + S - 1) / S;
     return S % MT == 0 && L >= 1 && L <= 9 && ni <= TEAM_NI_MAX;
-}
-// column-split teams (TeamArgs::xs): the column tiles [nt0, nt0 + ntn) of a GEMM with NT column tiles that XCD slot x
-// computes (balanced; a slot may get none)
-__host__ __device__ inline void team_xs_cols(int NT, int x, int& nt0, int& ntn) {
-    nt0 = x * NT / TEAM_MAX;
-    ntn = (x + 1) * NT / TEAM_MAX - nt0;
 }
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch

@@ -30,29 +30,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     warm_kernargs<10>();
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: keeps the k-loop scalar
-    // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin over the 8 XCDs,
-    // so XCD (bid % 8) gets a contiguous run of row-major tiles and its L2 serves their shared A rows
-    int bid = blockIdx.y * gridDim.x + blockIdx.x;
-    int n0, m0;
-    if ((g.swz & 15) == 2) {
-        // 2-D XCD partition (swz = 2 | RG << 4; the launcher picks RG x CG = 8 to minimise the fabric bytes
-        // M K CG + K N RG): XCD slot x = bid % 8 owns row-tile group x / CG and column-tile group x % CG, so each
-        // XCD fetches 1/RG of the A rows and 1/CG of the weights once instead of (1-D round-robin) all of one of them
-        const int RG = g.swz >> 4, CG = KSPLIT / RG;
-        const int MT = (g.M + BM - 1) / BM, NT = (g.N + BN - 1) / BN;
-        const int x = bid & 7, l = bid >> 3, rg = x / CG, cg = x % CG;
-        const int r0 = rg * MT / RG, r1 = (rg + 1) * MT / RG, c0 = cg * NT / CG, nc = (cg + 1) * NT / CG - c0;
-        if (nc <= 0 || l >= (r1 - r0) * nc) return;      // the grid is sized for the largest share
-        m0 = (r0 + l / nc) * BM;
-        n0 = (c0 + l % nc) * BN;
-    } else {
-        if (g.swz) {
-            const int full = (gridDim.x * gridDim.y) & ~7;
-            if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
-        }
-        n0 = (bid % gridDim.x) * BN;
-        m0 = (bid / gridDim.x) * BM;
-    }
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int n0 = (bid % gridDim.x) * BN;
+    const int m0 = (bid / gridDim.x) * BM;
     const int q4 = (lane >> 4) * 4;
 
     stamp_start(g.ts);
@@ -253,40 +233,15 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
     stamp_end(g.ts);
 }
 
-static int enc_swz() {   // LBIC_ENC_SWZ=1: XCD-aware tile order (off: with four workers' kernels interleaving on the
-                         // GPU, workgroups no longer land on XCDs in launch order; plain order 61.3 vs 60.6 Mpix/s);
-                         // 2: the 2-D XCD partition of row and column tiles (k_gemm)
-    const char* e = getenv("LBIC_ENC_SWZ");
-    return e ? atoi(e) : 0;
-}
-static const int g_enc_swz = enc_swz();
-static int enc_cfg() {
-    const char* e = getenv("LBIC_ENC_CFG");
-    return e ? atoi(e) : 0;
-}
-static const int g_enc_cfg = enc_cfg();
-static int small_max() {   // LBIC_SMALL_MAX: largest M for the small-M kernel (experiments)
-    const char* e = getenv("LBIC_SMALL_MAX");
-    return e ? atoi(e) : 64;
-}
-static const int g_small_max = small_max();
-static int dec_small_max() {   // LBIC_DEC_SMALL_MAX: largest M for the small-M kernel in decoder raster steps
-    const char* e = getenv("LBIC_DEC_SMALL_MAX");
-    return e ? atoi(e) : 1024;   // ganged raster passes of up to 32 batches of 32 images
-}
-static const int g_dec_small_max = dec_small_max();
+// largest M for the small-M kernel: the wavefront's ramp steps; a decoder raster step stays on it up to 1024 rows
+// (ganged raster passes of up to 32 batches of 32 images: a raster step's latency barely grows with its rows)
+constexpr int SMALL_MAX = 64, DEC_SMALL_MAX = 1024;
 
 // 0 = k_gemm_s (latency-shaped, any M; the decoder's raster steps stay on it when several batches are decoded
 // together: a raster step's latency barely grows with its rows), 1 = k_gemm (the encoder's wavefront steps)
 int gemm_class(const GemmArgs& g) {
-    return (g.M <= g_small_max || (g.raster && g.M <= g_dec_small_max)) ? 0 : 1;
+    return (g.M <= SMALL_MAX || (g.raster && g.M <= DEC_SMALL_MAX)) ? 0 : 1;
 }
-static int exact_on() {   // LBIC_EXACT=0: always load an (L+1)-th k-block (A/B experiments)
-    const char* e = getenv("LBIC_EXACT");
-    return e ? atoi(e) : 1;
-}
-static const int g_exact = exact_on();
-
 template <int BM, int BN, int NW, int CH, int OCC = 1>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
@@ -298,27 +253,7 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     }();
     (void)attr;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    GemmArgs gs = g;
-    gs.swz = g_enc_swz;
-    if (g_enc_swz == 2) {
-        // RG x CG = 8 minimising M K CG + K N RG (fabric bytes: every XCD reads its row group's A and column group's W)
-        const int MT = (g.M + BM - 1) / BM, NT = (g.N + BN - 1) / BN;
-        int best = 1;
-        double bc = 1e300;
-        for (int RG = 1; RG <= 8; RG *= 2) {
-            const double c = (double)g.M * (8 / RG) + (double)g.N * RG;
-            if (c < bc && MT >= RG && NT >= 8 / RG) { bc = c; best = RG; }
-        }
-        const int CG = 8 / best;
-        int most = 0;
-        for (int x = 0; x < 8; ++x) {
-            const int rg = x / CG, cg = x % CG;
-            most = std::max(most, ((rg + 1) * MT / best - rg * MT / best) * ((cg + 1) * NT / CG - cg * NT / CG));
-        }
-        gs.swz = 2 | (best << 4);
-        grid = dim3(8 * most, 1);
-    }
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, gs);
+    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, g);
     return launch_status("k_gemm");
 }
 
@@ -363,7 +298,7 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         const bool raster = (g.raster && g.ctr && g.need_blocks) || !g.need_blocks;
         if (g.raster && !g.ctr) return set_error(LBC_E_ARG, "raster GEMM needs the row counter");
         // every slice exactly L k-blocks: no (L+1)-th block to load (loads are what a launch waits for)
-        const bool exact = ((g.K >> 4) % KSPLIT) == 0 && g_exact;
+        const bool exact = ((g.K >> 4) % KSPLIT) == 0;
         const int sel = (raster ? 1 : 0) + (exact ? 2 : 0);
         switch ((g.K >> 4) / KSPLIT) {
 #define LBIC_V(L, R, E) hipLaunchKernelGGL((k_gemm_s<L, R, E>), grid, dim3(512), 0, s, g)
@@ -398,23 +333,9 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     // chunks 108.2 (round 2's earlier default, 86 VGPRs: 5 waves per SIMD, 2 beside the team decoder's 256 VGPRs);
     // 16x32 / 4 / 1 capped at 70 VGPRs 105.7; 32x32 / 8 / 1 107.5; 16x64 / 8 / 1 112.0; 16x16 / 4 / 1 122.3;
     // register caps that spill (64 / 80 VGPRs) 116.7 / 115.8.  Beside the team decoder (bench.py --steps 20):
-    // 84.9 Mpix/s against 79.7 for the earlier default.  LBIC_ENC_CFG selects the others for A/B runs.
-    switch (g_enc_cfg) {
-        case 1: return launch_cfg<64, 32, 4, 2>(g, s);
-        case 2: return launch_cfg<16, 32, 8, 2>(g, s);
-        case 3: return launch_cfg<32, 32, 8, 2>(g, s);
-        case 4: return launch_cfg<16, 32, 4, 1, 8>(g, s);     // <= 64 VGPRs (spills)
-        case 5: return launch_cfg<16, 32, 4, 2, 6>(g, s);     // <= 80 VGPRs (spills)
-        case 6: return launch_cfg<16, 32, 4, 1, 6>(g, s);
-        case 8: return launch_cfg<16, 32, 4, 1, 1>(g, s);
-        case 9: return launch_cfg<32, 32, 4, 1, 1>(g, s);
-        case 10: return launch_cfg<16, 64, 4, 1, 1>(g, s);
-        case 11: return launch_cfg<16, 16, 4, 1, 1>(g, s);
-        case 12: return launch_cfg<16, 64, 8, 1, 1>(g, s);
-        case 13: return launch_cfg<32, 32, 8, 1, 1>(g, s);
-        case 15: return launch_cfg<16, 32, 4, 2>(g, s);
-        default: return launch_cfg<16, 32, 8, 1>(g, s);    // 0 and 7
-    }
+    // 84.9 Mpix/s against 79.7 for the earlier default.  (Other tiles, XCD-aware and 2-D XCD tile orders: measured
+    // in rounds 2-3 and removed)
+    return launch_cfg<16, 32, 8, 1>(g, s);
 }
 
 

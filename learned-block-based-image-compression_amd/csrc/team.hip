@@ -142,13 +142,7 @@ template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
                                                 float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
-#if defined(LBIC_TEAM_DEEP) && LBIC_TEAM_DEEP == 2
-    constexpr bool PF = true, PF2 = true;        // experiment: items j + 1 and j + 2 in flight during item j's chain
-#elif defined(LBIC_TEAM_DEEP)
-    constexpr bool PF = true, PF2 = false;       // experiment: the next item in flight at every slice length
-#else
-    constexpr bool PF = LL <= 7, PF2 = false;    // prefetch the next item's fragments
-#endif
+    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
     constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -213,21 +207,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         dstamp(dts, 1, 0.f);
         // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
         // hit) so that no load sits behind a branch
-        if constexpr (PF2) {
-            f4 w2[LL];
-            issue(min(1, ni - 1), w1);
-            for (int j = 0;;) {
-                issue(min(j + 2, ni - 1), w2);
-                chain(j, w0);
-                if (++j >= ni) break;
-                issue(min(j + 2, ni - 1), w0);
-                chain(j, w1);
-                if (++j >= ni) break;
-                issue(min(j + 2, ni - 1), w1);
-                chain(j, w2);
-                if (++j >= ni) break;
-            }
-        } else if constexpr (PF) {
+        if constexpr (PF) {
             for (int j = 0;;) {
                 issue(min(j + 1, ni - 1), w1);
                 chain(j, w0);
@@ -262,18 +242,17 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     dstamp(dts, 4, 0.f);
 }
 
-// The output tiles of g this workgroup computes: rank `rank` of the S workgroups that share column tiles
-// [nt0, nt0 + ntn) (the whole GEMM, or -- column-split teams -- the range of this workgroup's XCD slot)
-__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn,
-                                              float* red, bool wt, int ph = 0, int wy = 0,
-                                              unsigned long long* dts = nullptr) {
+// The output tiles of g this workgroup computes: rank `rank` of the team's S workgroups
+__device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
+                                              int ph = 0, int wy = 0, unsigned long long* dts = nullptr) {
+    const int nt0 = 0, ntn = (g.N + 15) >> 4;
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
     const bool exact = (nkb % KSPLIT) == 0;
     const int MT = (g.M + 15) >> 4, items = MT * ntn;
     const int ni = rank < items ? (items - rank + S - 1) / S : 0;
     if (ni == 0) return;
-    if (team_fast_path(g, S, ntn)) {
+    if (team_fast_path(g, S)) {
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                          \
     case L_ * 2 + 1:                                                                                        \
@@ -293,74 +272,14 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     team_gemm_long(g, v, h, rank, S, nt0, ntn, red, wt);
 }
 
-// The weight fragments of the first NIT items this workgroup computes in GEMM g (each wave: its K slice), requested
-// while the workgroup waits at the team barrier in front of g (weights are read-only: no ordering against the
-// barrier is needed).  The values are folded into one LDS word nobody reads, so the loads are kept; the wave waits
-// for them at the barrier's closing __syncthreads, i.e. crossing the barrier costs max(barrier, fetch).
-template <int NIT>
-__device__ __forceinline__ void team_prefetch(const GemmArgs& g, int rank, int S, float* sink) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nkb = g.K >> 4;
-    const int kb0 = wave * nkb / KSPLIT, kb1 = (wave + 1) * nkb / KSPLIT;
-    const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
-    f4 w[NIT][10];
-#pragma unroll
-    for (int j = 0; j < NIT; ++j) {
-        const int nt = min(rank + j * S, items - 1) / MT;
-#pragma unroll
-        for (int c = 0; c < 10; ++c) w[j][c] = Wt[((long)min(kb0 + c, kb1 - 1) * g.NB16 + nt) * 64];
-    }
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < NIT; ++j)
-#pragma unroll
-        for (int c = 0; c < 10; ++c) s += w[j][c][0];
-    if (lane == 0) sink[wave] = s;
-}
-
-__device__ __forceinline__ void team_prefetch_any(const GemmArgs* g, int rank, int S, int nit, float* sink) {
-    if (!g || rank >= (((g->M + 15) >> 4) * ((g->N + 15) >> 4))) return;
-    if (nit >= 2) team_prefetch<2>(*g, rank, S, sink);
-    else team_prefetch<1>(*g, rank, S, sink);
-}
-
-// wait (one lane polls, relaxed, s_sleep between polls, bounded) until *c >= target; false: the launch failed
-__device__ __forceinline__ bool team_wait(unsigned* c, unsigned target, unsigned* fail, unsigned long long tmo,
-                                          int* sflag) {
-    if (threadIdx.x == 0) {
-        int f = 0;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load((gptr<unsigned>)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                f = 1;
-                break;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-                __hip_atomic_store((gptr<unsigned>)fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                f = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        *sflag = f;
-    }
-    __syncthreads();
-    return *sflag == 0;
-}
-
-// team barrier number `epoch` (1, 2, ...): every wave's stores drained, one arrival per workgroup, one lane polls
-// (relaxed, s_sleep between polls, bounded); false: the launch failed (timeout here or anywhere else).  pf: the next
-// GEMM, whose first weight tiles are requested after the arrival (team_prefetch)
+// team barrier: every wave's stores drained, one arrival per workgroup, one lane polls (relaxed, s_sleep between
+// polls, bounded); false: the launch failed (timeout here or anywhere else)
 __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
-                                          int* sflag, const GemmArgs* pf = nullptr, int rank = 0, int S = 1,
-                                          int npf = 0, float* sink = nullptr) {
+                                          int* sflag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (npf) team_prefetch_any(pf, rank, S, npf, sink);
     if (threadIdx.x == 0) {
         int f = 0;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -390,57 +309,27 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch.
 // DENSE (TeamArgs::dense): the high-rate instance, tables staged in LDS and rans_row<true>; a separate instance so the
 // low-rate one keeps its register allocation.
-#if defined(LBIC_TEAM_DEEP) && LBIC_TEAM_DEEP == 2
-#define LBIC_TEAM_OCC 2
-#elif defined(LBIC_TEAM_DEEP)
-#define LBIC_TEAM_OCC 3
-#else
-#define LBIC_TEAM_OCC 4
-#endif
-template <int MODE>
-__global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs ta) {
-    constexpr bool DENSE = MODE == 1;
+template <bool DENSE>
+__global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host for the step's largest per-workgroup tile count (TeamArgs::ni_max):
-    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][barrier flag, padded to 16 B][8 prefetch sink words]
+    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][barrier flag, padded to 16 B]
     // [GEMM partials ni_max x KSPLIT x 256 floats]
     // [dense rANS only: the table image, total16 16-bit entries]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
     uint32_t* lwin = team_lds;
     uint32_t* rcache = team_lds + RANS_WIN;                              // rans_row_sparse<.., true>'s state cache
     int& sflag = *reinterpret_cast<int*>(team_lds + RANS_WIN + RC_WORDS);
-    float* sink = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 4);     // team_prefetch's unread word per wave
-    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 12);
+    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + 4);
     if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
     // spread 2 (at most four teams): team t = the workgroups of slots 2t and 2t + 1 (two XCDs), ranks interleaved
-    // xs (column-split): grid = 8 x T W; team t = the W workgroups q = blockIdx / 8 in [t W, (t + 1) W) of every slot,
-    // rank = slot W + q % W; in a GEMM the W workgroups of slot x share the column tiles team_xs_cols(x)
-    if (ta.prio == 1) __builtin_amdgcn_s_setprio(1);
-    else if (ta.prio == 2) __builtin_amdgcn_s_setprio(2);
-    else if (ta.prio >= 3) __builtin_amdgcn_s_setprio(3);
     const int slot = blockIdx.x & 7;
-    int team, rank;
-    if (ta.xs) {
-        const int q = blockIdx.x >> 3;
-        team = q / ta.W;
-        rank = slot * ta.W + q % ta.W;
-    } else {
-        team = ta.spread == 2 ? slot >> 1 : slot;
-        rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
-    }
+    const int team = ta.spread == 2 ? slot >> 1 : slot;
+    const int rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
     if (team >= T || rank >= S) return;
-    // the GEMM tile share of this workgroup: rank grk of gS over the column tiles of its slot (xs) or of the GEMM
-    const int grk = ta.xs ? rank % ta.W : rank, gS = ta.xs ? ta.W : S;
-    auto cols = [&](const GemmArgs& g, int& nt0, int& ntn) {
-        const int NT = (g.N + 15) >> 4;
-        if (ta.xs) team_xs_cols(NT, slot, nt0, ntn);
-        else { nt0 = 0; ntn = NT; }
-    };
-    // row-tile groups: the ranks r % ngr == grp of the team (ngr = ta.groups; 1 = the whole team) share a barrier counter
-    const int ngr = ta.xs ? 1 : max(ta.groups, 1), grp = rank % ngr, gsz = S / ngr;
-    unsigned* ctr = ta.sync + team * 32 + (ngr > 1 ? 2 + grp : 0);
+    unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -455,7 +344,7 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
     unsigned long long* tsr = ta.ts ? ta.ts + team * 256 : nullptr;   // every rank: [160 + rank] rANS done, [192 + rank]
                                                                        // the GEMM waves beside it done (sampled step)
     if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
-    if (MODE != 0) {     // the rANS tables, once per launch (read-only: no hand-off); the census barrier's
+    if constexpr (DENSE) {     // the rANS tables, once per launch (read-only: no hand-off); the census barrier's
         const uint4* src = reinterpret_cast<const uint4*>(R.cdf16);      // __syncthreads (or the one below) orders them
         uint4* dst = reinterpret_cast<uint4*>(tab);
         for (int i = threadIdx.x; i < R.total16 / 8; i += blockDim.x) dst[i] = src[i];
@@ -467,7 +356,8 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
         // placement census: every workgroup ORs its XCD into its team's word [1], then a barrier over the whole
         // grid (counter [T * 32 + 1]); any team on more than one XCD -> every workgroup leaves
         if (threadIdx.x == 0)
-            __hip_atomic_fetch_or((gptr<unsigned>)(ctr + 1), 1u << xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or((gptr<unsigned>)(ta.sync + team * 32 + 1), 1u << xcc_id(), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
         if (!team_sync(ta.sync + T * 32 + 1, (unsigned)(T * S), fail, ta.tmo, &sflag)) return;
         bool local = true;
         for (int t = 0; t < T; ++t)
@@ -486,76 +376,43 @@ __global__ __launch_bounds__(512, LBIC_TEAM_OCC) void k_dec_team(const TeamArgs 
                 const int k = ta.opk[op];
                 if (k >= 0) {
                     const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + k);
-                    int nt0, ntn;
-                    cols(g, nt0, ntn);
-                    team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
+                    team_gemm_any(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
                                   samp ? ts + 64 + op * 8 : nullptr);
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
                     const bool sstep = tsr && v == ta.sv && h == ta.sh && rank < 32;
                     if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
-                        // rows: every image of the batch (ngr = 1), or the images of this group's row tile
-                        const int r0 = ngr > 1 ? 16 * grp + rank / ngr : rank, rs = ngr > 1 ? gsz : S;
-                        const int r1 = ngr > 1 ? min(16 * grp + 16, R.rows) : R.rows;
-                        if (!DENSE && ta.rpersist && r0 < r1 && r0 + rs >= r1) {
+                        if (!DENSE && rank < R.rows && rank + S >= R.rows) {
                             // one image per workgroup, the same one at every step: the coder state stays in LDS
-                            if constexpr (MODE == 2) rans_row_sparse<true, true>(R, lwin, r0, lane, wt, tab, rcache);
-                            else if constexpr (!DENSE) rans_row_sparse<true, true>(R, lwin, r0, lane, wt, nullptr, rcache);
+                            rans_row_sparse<true, true>(R, lwin, rank, lane, wt, nullptr, rcache);
                         } else {
-                            for (int r = r0; r < r1; r += rs) {
+                            for (int r = rank; r < R.rows; r += S) {
                                 if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
-                                else if constexpr (MODE == 2) rans_row_sparse<true>(R, lwin, r, lane, wt, tab);
                                 else rans_row_sparse<true>(R, lwin, r, lane, wt);
                             }
                         }
                         if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
-                        int nt0, ntn;
-                        cols(g, nt0, ntn);
-                        team_gemm_any(g, v, h, grk, gS, nt0, ntn, red, wt, 1, ta.split_wy);
+                        team_gemm_any(g, v, h, rank, S, red, wt, 1, ta.split_wy);
                         if (sstep && threadIdx.x == 0) tsr[192 + rank] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
-                target += gsz;
-                const GemmArgs* nx = nullptr;
-                if (ta.pf) {     // the GEMM after this barrier (the next step's first at the step's end)
-                    int nop = op + 1, ncls = cls;
-                    if (nop == ta.nops) {
-                        nop = 0;
-                        const int hn = h + 1 == ta.Wb ? 0 : h + 1;
-                        ncls = hn == 0 ? 0 : hn == ta.Wb - 1 ? 2 : 1;
-                    }
-                    if (ta.opk[nop] >= 0) nx = (const GemmArgs*)(G + ncls * ta.NG + ta.opk[nop]);
-                }
-                if (!team_sync(ctr, target, fail, ta.tmo, &sflag, nx, rank, S, ta.pf, sink)) return;
+                target += S;
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
                 if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
             }
             if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
             if (ts && v == ta.sv && h == ta.sh - 1 && threadIdx.x == 0) ts[60] = __builtin_amdgcn_s_memrealtime();
-            if (ta.align) {
-                // cross-team step alignment (column-split teams: the teams on an XCD read the same weight slice, which
-                // stays in its L2 only while they run the same operation at about the same time).  The team's rank 0
-                // counts the finished step on one launch-wide counter; every workgroup then waits until every team has
-                // finished step s + 1 - lag (align 2: lag 0, lockstep; align 1: lag 1, at most one step apart)
-                unsigned* gctr = ta.sync + (TEAM_MAX + 1) * 32;
-                const unsigned sidx = (unsigned)(v * ta.Wb + h);
-                if (rank == 0 && threadIdx.x == 0)
-                    __hip_atomic_fetch_add((gptr<unsigned>)gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned need = (unsigned)T * (sidx + (ta.align == 2 ? 1u : 0u));
-                if (need && !team_wait(gctr, need, fail, ta.tmo, &sflag)) return;
-            }
         }
     }
     if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
 }
 
 static const void* team_instance(int dense) {
-    return dense == 1   ? reinterpret_cast<const void*>(&k_dec_team<1>)
-           : dense == 2 ? reinterpret_cast<const void*>(&k_dec_team<2>)
-                        : reinterpret_cast<const void*>(&k_dec_team<0>);
+    return dense ? reinterpret_cast<const void*>(&k_dec_team<true>) : reinterpret_cast<const void*>(&k_dec_team<false>);
 }
 
 int team_blocks_per_cu(int dense, size_t lds) {
@@ -567,7 +424,7 @@ int team_blocks_per_cu(int dense, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + RC_WORDS + 12) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
+    return (size_t)(RANS_WIN + RC_WORDS + 4) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 + (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
@@ -575,7 +432,7 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
         return set_error(LBC_E_ARG, "bad team decoder arguments");
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
     static const bool attr = [] {
-        for (int d = 0; d < 3; ++d)
+        for (int d = 0; d < 2; ++d)
             (void)hipFuncSetAttribute(team_instance(d), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -584,12 +441,9 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
     if (a.spread != 1 && (a.spread != 2 || a.T > TEAM_MAX / 2 || a.S % 2 || a.plain))
         return set_error(LBC_E_ARG, "bad team spread");
-    if (a.xs && (a.W < 1 || a.S != 8 * a.W || a.plain || a.spread != 1 || a.pf))
-        return set_error(LBC_E_ARG, "bad column-split team geometry");
-    const dim3 grid(a.xs ? 8 * a.T * a.W : 8 * a.S / a.spread);
-    if (a.dense == 1) hipLaunchKernelGGL(k_dec_team<1>, grid, dim3(512), lds, s, a);
-    else if (a.dense == 2) hipLaunchKernelGGL(k_dec_team<2>, grid, dim3(512), lds, s, a);
-    else hipLaunchKernelGGL(k_dec_team<0>, grid, dim3(512), lds, s, a);
+    const dim3 grid(8 * a.S / a.spread);
+    if (a.dense) hipLaunchKernelGGL(k_dec_team<true>, grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_team<false>, grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

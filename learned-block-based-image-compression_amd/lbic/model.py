@@ -242,23 +242,20 @@ class BlockBasedImgCompLossyNetv9:
 
     def team_stats(self):
         """The last decompress_teams launch led by this handle (lbc_team_stats): dict(launch_ms, bytes, flops,
-        plain, mode, sc1_reruns, timeout_fallbacks, column_split) -- its duration, algorithmic bytes / FLOPs, the
-        hand-off store mode it ran in, how the call decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant,
-        or "fallback" to lbc_decode per batch), and the handle's event counters (lbc_team_events): write-through
-        reruns, barrier timeouts decoded through the fallback, whether the last launch ran column-split; its layout
-        (lbc_team_layout): row-tile groups and whether the sparse rANS searched an LDS table copy."""
+        plain, mode, sc1_reruns, timeout_fallbacks) -- its duration, algorithmic bytes / FLOPs, the hand-off store mode
+        it ran in, how the call decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant, or "fallback" to
+        lbc_decode per batch), and the handle's event counters (lbc_team_events): write-through reruns and barrier
+        timeouts decoded through the fallback."""
         L = _lib.lib()
         ms, by, fl, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         _lib.check(L.lbc_team_stats(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(fl), ctypes.byref(pl)))
         mode = ctypes.c_int()
         _lib.check(L.lbc_team_mode(self._h, ctypes.byref(mode)))
-        rr, to, xs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        _lib.check(L.lbc_team_events(self._h, ctypes.byref(rr), ctypes.byref(to), ctypes.byref(xs)))
-        gr, sl = ctypes.c_int(), ctypes.c_int()
-        _lib.check(L.lbc_team_layout(self._h, ctypes.byref(gr), ctypes.byref(sl)))
+        rr, to = ctypes.c_int(), ctypes.c_int()
+        _lib.check(L.lbc_team_events(self._h, ctypes.byref(rr), ctypes.byref(to)))
         return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value,
                     mode=("fallback", "team_sparse", "team_dense")[mode.value], sc1_reruns=rr.value,
-                    timeout_fallbacks=to.value, column_split=xs.value, groups=gr.value, sparse_lds_tables=sl.value)
+                    timeout_fallbacks=to.value)
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]
@@ -370,8 +367,7 @@ def decompress_teams(models: Sequence["BlockBasedImgCompLossyNetv9"], batches: S
     Hb x Wb blocks.  Returns [zhat_t [n, Hb, Wb, 3B^2]], bit-identical to models[t].decompress_batch(batches[t]).
     wg_per_cu (LBC_OPT_TEAM_WG_PER_CU): 1 leaves room for an encoder running beside the launch; 2 doubles each
     team's workgroups (every register of the GPU) for a decode with the GPU otherwise idle.  team_size
-    (LBC_OPT_TEAM_SIZE): workgroups per team, 0 = one per CU of an XCD; fewer for a launch on a stream restricted to
-    that many CUs per XCD (lbic.streams.cu_split_streams)."""
+    (LBC_OPT_TEAM_SIZE): workgroups per team, 0 = one per CU of an XCD; fewer: small teams."""
     T = len(batches)
     if T < 1 or T > 8 or len(models) < T:
         raise ValueError("1 to 8 batches, one model handle each")

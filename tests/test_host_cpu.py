@@ -106,23 +106,3 @@ def test_transform_weights_are_a_codec():
     assert psnr > 28 and bpp < 1.5, (psnr, bpp)
     with pytest.raises(ValueError):
         transform_state_dict(Arch(4, (3, 3, 1, 1), 512, 96))    # 96 coefficients > 3 * 4^2
-
-
-def test_cu_split_masks():
-    """bench.py --dec-cus: the decoder's and the encoder's CU masks are disjoint, cover every CU, give every XCD
-    (bit i -> XCD i % 8, slot i // 8) the requested count, and keep both sides on every XCD under the other
-    conceivable bit order too (bit i -> XCD i // 32): each holds a slot of every group of four consecutive slots."""
-    from lbic.streams import split_slots, xcd_slot_mask
-    for K in (8, 12, 16, 20, 24):
-        dec, enc = split_slots(32, K)
-        assert len(dec) == K and not dec & enc and dec | enc == set(range(32))
-        md, me = xcd_slot_mask(256, dec), xcd_slot_mask(256, enc)
-        assert all((a & b) == 0 and (a | b) == 0xFFFFFFFF for a, b in zip(md, me))
-        for x in range(8):
-            assert sum(1 for i in range(256) if i % 8 == x and md[i // 32] >> (i % 32) & 1) == K
-            for m in (md, me):
-                assert any(m[x] >> c & 1 for c in range(32))          # blocked order: XCD x = word x
-        for g in range(8):
-            assert dec & set(range(4 * g, 4 * g + 4)) and enc & set(range(4 * g, 4 * g + 4))
-    with pytest.raises(ValueError):
-        xcd_slot_mask(256, {32})

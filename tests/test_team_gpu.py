@@ -55,23 +55,21 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
     return ref, got, hs, st
 
 
-@pytest.mark.parametrize("xs", [0, 1])
 @pytest.mark.parametrize("name,T,n,shape", [
     ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
     ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)), ("b8_lowrate_2rows", 5, 48, (2, 9)),
+    ("b8_lowrate_2rows", 8, 64, (2, 5)),
 ])
-def test_team_equals_graph_decoder(name, T, n, shape, xs, monkeypatch):
-    """xs = 1: column-split teams (LBIC_TEAM_XS=1; every team spans the eight XCD slots, each slot a fixed eighth of
-    every GEMM's column tiles) -- the same results."""
+def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
+    """Image counts of one, two, three and four row tiles, 1-8 teams."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     g = load_golden("loop_" + name)
     Hb, Wb = shape or g["x"].shape[:2]
     ref, got, hs, _ = run_case(name, T, n, Hb, Wb, seed=T * 7 + n)
     for t in range(T):
         assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
     st = hs[0].team_stats()
-    assert st["mode"] == "team_sparse" and st["column_split"] == xs
+    assert st["mode"] == "team_sparse"
 
 
 @pytest.mark.parametrize("name,T,n,shape", [("tiny_ks3311", 3, 5, (3, 4)), ("b8_lowrate_2rows", 4, 32, (2, 24))])
@@ -85,13 +83,11 @@ def test_team_write_through_mode(name, T, n, shape, monkeypatch):
         assert torch.equal(got[t], ref[t])
 
 
-@pytest.mark.parametrize("xs", [0, 1])
 @pytest.mark.parametrize("shape", [(1, 1), (1, 9), (7, 1), (3, 5), (2, 2)])
-def test_team_ragged_frames_ks3311(shape, xs, monkeypatch):
+def test_team_ragged_frames_ks3311(shape, monkeypatch):
     """One block, one row, one column, odd rectangles: the three column classes of the KS3311 step (layer-0 cache
     border cells at h = 0 and h = Wb - 1, both at once when Wb = 1)."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     ref, got, _, _ = run_case("tiny_ks3311", 3, 2, *shape, seed=sum(shape))
     for t in range(3):
         assert torch.equal(got[t], ref[t])
@@ -132,52 +128,24 @@ def test_team_spread_two_xcds(name, T, n, shape, spread, monkeypatch):
 
 @pytest.mark.parametrize("S", [1, 3, 7])
 def test_team_small_teams(S, monkeypatch):
-    """Teams of 1, 3 and 7 workgroups: every workgroup walks many output tiles per GEMM (the weight-prefetch loop,
-    row tiles changing between items) and decodes several rANS streams per step."""
+    """Teams of 1, 3 and 7 workgroups (LBC_OPT_TEAM_SIZE): every workgroup walks many output tiles per GEMM (the
+    weight-prefetch loop, row tiles changing between items) and decodes several rANS streams per step."""
+    from lbic.model import decompress_teams
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    monkeypatch.setenv("LBIC_TEAM_S", str(S))
-    ref, got, _, _ = run_case("b8_lowrate_2rows", 2, 35, 2, 6, seed=S)
+    monkeypatch.setenv("LBIC_TEAM_SPREAD", "1")
+    ref, _, hs, st = run_case("b8_lowrate_2rows", 2, 35, 2, 6, seed=S)
+    got = decompress_teams(hs, st, 2, 6, team_size=S)
     for t in range(2):
         assert torch.equal(got[t], ref[t])
-
-
-@pytest.mark.parametrize("K", [8, 16])
-def test_team_on_cu_masked_stream(K, monkeypatch):
-    """bench.py --dec-cus: a team launch with teams of K workgroups (LBC_OPT_TEAM_SIZE) on a stream restricted to K
-    CUs of every XCD (hipExtStreamCreateWithCUMask), while the encoder codes the next batch on a stream holding the
-    other CUs -- the same results as the graph decoder, and the encoder's results unchanged."""
-    from lbic.model import decompress_teams
-    from lbic.streams import cu_split_streams
-    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    dev = torch.device("cuda", 0)
-    s_enc, s_dec = cu_split_streams(K, dev)
-    ref, _, hs, st = run_case("b8_lowrate_2rows", 3, 32, 2, 24, seed=K)
-    arch = golden_arch(load_golden("loop_b8_lowrate_2rows"))
-    x = batches(arch, 1, 32, 2, 24, seed=K + 1)[0]
-    want = hs[0].compress_batch(x)
-    torch.cuda.synchronize()
-    with torch.cuda.stream(s_enc):
-        enc = hs[0].compress_batch(x)
-    with torch.cuda.stream(s_dec):
-        got = decompress_teams(hs, st, 2, 24, team_size=K)
-        s_dec.synchronize()
-    s_enc.synchronize()
-    for t in range(3):
-        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
-    for k in ("symbols", "indexes", "zhat"):
-        assert torch.equal(enc[k], want[k])
-    assert hs[0].team_stats()["mode"] == "team_sparse"
 
 
 @pytest.mark.parametrize("name,T,n,shape,scale", [
     ("tiny_ks3111", 3, 5, None, 0.05), ("tiny_ks3311", 8, 3, None, 0.05), ("b8_lowrate_2rows", 4, 32, (2, 24), 0.05),
     ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
-@pytest.mark.parametrize("xs", [0, 1])
-def test_team_dense_rans(name, T, n, shape, scale, xs, monkeypatch):
+def test_team_dense_rans(name, T, n, shape, scale, monkeypatch):
     """The dense rANS variant inside the team kernel (high rates; every workgroup stages the tables in its LDS once per
     launch, one wave per stream runs rans_row<true>): forced by LBIC_RANS_SPARSE=0 at the fixtures' low rates, and
     picked by rate (>= 1 bit per symbol, bypass escapes included) on high-amplitude batches."""
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     if scale < 1:
         monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
     else:
@@ -228,13 +196,11 @@ def test_team_stamps(monkeypatch):
         assert row[63] > row[62] > 0 and row[61] > row[60] > 0
 
 
-@pytest.mark.parametrize("xs", [0, 1])
-def test_team_barrier_timeout_falls_back(xs, monkeypatch):
+def test_team_barrier_timeout_falls_back(monkeypatch):
     """A team barrier that times out (forced: LBIC_TEAM_TMO=1 tick) ends the launch on every workgroup; the batches are
     then decoded through lbc_decode one after another in the same call, with the same results, and the event is
     counted (lbc_team_events) instead of failing the decode."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     _, hs0 = handles("b8_lowrate_2rows", 1)
     before = hs0[0].team_stats()["timeout_fallbacks"]
     monkeypatch.setenv("LBIC_TEAM_TMO", "1")
@@ -256,7 +222,6 @@ def test_team_dense_two_workgroups_per_cu(monkeypatch):
     such workgroups do not fit one CU's LDS, so the launch must shrink to one per CU (occupancy query on the dense
     instance with the launch's dynamic LDS) rather than start a grid that cannot be co-resident."""
     monkeypatch.delenv("LBIC_RANS_SPARSE", raising=False)
-    monkeypatch.delenv("LBIC_TEAM_XS", raising=False)
     _, hs0 = handles("b8_lowrate_2rows", 1)
     before = hs0[0].team_stats()["timeout_fallbacks"]      # (a per-handle counter: earlier tests may have counted)
     ref, got, hs, _ = run_case("b8_lowrate_2rows", 8, 32, 2, 7, seed=21, scale=4.0, wpc=2)
@@ -264,51 +229,3 @@ def test_team_dense_two_workgroups_per_cu(monkeypatch):
         assert torch.equal(got[t], ref[t])
     st = hs[0].team_stats()
     assert st["mode"] == "team_dense" and st["timeout_fallbacks"] == before, st
-
-
-@pytest.mark.parametrize("xs,align", [(1, 1), (1, 2), (0, 2)])
-def test_team_step_alignment(xs, align, monkeypatch):
-    """LBIC_TEAM_ALIGN (cross-team step alignment: 1 = teams at most one raster step apart, 2 = lockstep) changes only
-    when teams start a step, never what they compute."""
-    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
-    monkeypatch.setenv("LBIC_TEAM_ALIGN", str(align))
-    ref, got, hs, _ = run_case("b8_lowrate_2rows", 6, 32, 2, 10, seed=31)
-    for t in range(6):
-        assert torch.equal(got[t], ref[t])
-    assert hs[0].team_stats()["mode"] == "team_sparse"
-
-
-@pytest.mark.parametrize("sparse_lds", [0, 1])
-@pytest.mark.parametrize("name,T,n,shape,groups", [
-    ("b8_lowrate_2rows", 8, 32, (2, 96), 2), ("b8_lowrate_2rows", 3, 64, (2, 20), 4),
-    ("tiny_ks3311", 2, 20, (3, 4), 1), ("tiny_ks3111", 2, 20, None, 2), ("b8_lowrate_2rows", 2, 40, (2, 20), 1),
-    ("tiny_ks3111", 1, 4, None, 1),
-])
-def test_team_row_groups(name, T, n, shape, groups, sparse_lds, monkeypatch):
-    """LBIC_TEAM_GROUPS=1: the team split into one barrier group per 16-image row tile (each group decodes the rANS
-    rows of its own images); 40 images (three row tiles) on 64 workgroups, 4 images (one row tile) and KS3311 (the
-    layer-0 cache GEMM has a row per cell, not per image) keep one group.
-    LBIC_TEAM_SPARSE_LDS=1: the sparse rANS searches its far symbols in an LDS copy of the table image.  Same results
-    as the graph decoder."""
-    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    monkeypatch.setenv("LBIC_TEAM_GROUPS", "1")
-    monkeypatch.setenv("LBIC_TEAM_SPARSE_LDS", str(sparse_lds))
-    g = load_golden("loop_" + name)
-    Hb, Wb = shape or g["x"].shape[:2]
-    ref, got, hs, _ = run_case(name, T, n, Hb, Wb, seed=T * 11 + n)
-    for t in range(T):
-        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
-    st = hs[0].team_stats()
-    assert st["mode"] == "team_sparse" and st["groups"] == groups and st["sparse_lds_tables"] == sparse_lds
-
-
-def test_team_row_groups_dense(monkeypatch):
-    """Row-tile groups with the dense rANS variant (tables in LDS) on streams coded at high amplitude."""
-    monkeypatch.setenv("LBIC_RANS_SPARSE", "0")
-    monkeypatch.setenv("LBIC_TEAM_GROUPS", "1")
-    ref, got, hs, _ = run_case("b8_lowrate_2rows", 2, 32, 2, 24, seed=5, scale=0.5)
-    for t in range(2):
-        assert torch.equal(got[t], ref[t])
-    st = hs[0].team_stats()
-    assert st["mode"] == "team_dense" and st["groups"] == 2

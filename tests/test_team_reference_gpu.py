@@ -4,8 +4,8 @@
   decompress() (graphs/models/BlockBasedImgCompLossy_net.py:400-452) produced from the reference's stream of the
   fixture's symbols.  That stream is re-made here by the oracle coder (oracle/rans_oracle.c, byte-identical to the
   product coder: tests/test_gpu_parity.py) from the fixture's symbols and indexes, and decoded by team launches --
-  copies of it in every image slot of several teams, both team geometries (one XCD slot per team, and column-split
-  teams that span all eight slots) and both rANS variants.  Every decoded image must equal ``zhat_dec`` within 1e-5
+  copies of it in every image slot of several teams, both team geometries (one XCD slot per team, and teams of two
+  XCD slots with write-through hand-offs) and both rANS variants.  Every decoded image must equal ``zhat_dec`` within 1e-5
   relative (north_star's bar) and be bit-identical across copies.
 * The full 768x768 B8_lowrate frame (frame_b8_lowrate.npz, the reference's compress() closed loop) inside a launch of
   the headline's shape: 8 teams x 32 frames of 768x768.  Team t carries the fixture's stream in image slot t and 31
@@ -47,13 +47,13 @@ def _handles(arch, seed, rate, T):
     return hs[:T]
 
 
-@pytest.mark.parametrize("xs", [0, 1])
+@pytest.mark.parametrize("spread", [1, 2])
 @pytest.mark.parametrize("sparse", ["0", "1"])
 @pytest.mark.parametrize("name", LOOPS)
-def test_team_decodes_reference_stream(name, sparse, xs, monkeypatch):
+def test_team_decodes_reference_stream(name, sparse, spread, monkeypatch):
     from lbic.model import decompress_teams
     monkeypatch.setenv("LBIC_RANS_SPARSE", sparse)
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
+    monkeypatch.setenv("LBIC_TEAM_SPREAD", str(spread))
     g = load_golden("loop_" + name)
     arch = golden_arch(g)
     Hb, Wb = g["x"].shape[:2]
@@ -63,7 +63,7 @@ def test_team_decodes_reference_stream(name, sparse, xs, monkeypatch):
     got = decompress_teams(hs, [[stream] * n for _ in range(T)], Hb, Wb)
     st = hs[0].team_stats()
     assert st["mode"] == ("team_sparse" if sparse == "1" else "team_dense"), st
-    assert st["column_split"] == xs
+    assert st["plain"] == (1 if spread == 1 else 0), st
     ref = g["zhat_dec"]
     worst = 0.0
     for t in range(T):
@@ -72,14 +72,12 @@ def test_team_decodes_reference_stream(name, sparse, xs, monkeypatch):
             assert torch.equal(got[t][i], got[0][0]), f"team {t} image {i} differs from team 0 image 0"
             assert_rel(z, ref, what=f"team {t} image {i} vs the reference's decompress()")
             worst = max(worst, float(np.abs(z - ref).max()))
-    print(f"{name} xs={xs} sparse={sparse}: max |zhat - zhat_dec(ref)| = {worst:.3e} (bar {1e-5 * np.abs(ref).max():.3e})")
+    print(f"{name} spread={spread} sparse={sparse}: max |zhat - zhat_dec(ref)| = {worst:.3e} (bar {1e-5 * np.abs(ref).max():.3e})")
 
 
-@pytest.mark.parametrize("xs", [0, 1])
-def test_team_full_frame_in_headline_launch(xs, monkeypatch):
+def test_team_full_frame_in_headline_launch(monkeypatch):
     from lbic.layout import image_to_blocks
     from lbic.model import decompress_teams
-    monkeypatch.setenv("LBIC_TEAM_XS", str(xs))
     monkeypatch.delenv("LBIC_RANS_SPARSE", raising=False)
     g = load_golden("frame_b8_lowrate")
     arch = golden_arch(g)
@@ -112,7 +110,7 @@ def test_team_full_frame_in_headline_launch(xs, monkeypatch):
         owners.append(order[:t] + [-1] + order[t:])
     got = decompress_teams(hs, batches, Hb, Wb)
     st = hs[0].team_stats()
-    assert st["mode"] == "team_sparse" and st["column_split"] == xs, st
+    assert st["mode"] == "team_sparse", st
     rows, zr = g["zhat_rows"], g["zhat_row_data"]
     for t in range(T):
         for i, k in enumerate(owners[t]):
@@ -124,5 +122,5 @@ def test_team_full_frame_in_headline_launch(xs, monkeypatch):
         assert dz <= 1e-5 * float(np.abs(zr).max()), f"team {t}: zhat rows differ from the reference by {dz}"
         assert dsum <= 1e-5 * float(np.abs(z).sum(-1).max()), f"team {t}: block sums differ by {dsum}"
         assert torch.equal(got[t][t], r["zhat"][0])
-    print(f"headline launch xs={xs}: fixture frame in 8 teams, max |dzhat| rows {dz:.3e}, block sums {dsum:.3e}, "
+    print(f"headline launch: fixture frame in 8 teams, max |dzhat| rows {dz:.3e}, block sums {dsum:.3e}, "
           f"{len(flips)} scale-index flips at listed near ties")
