@@ -182,6 +182,8 @@ struct lbc_model {
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
     int team_wpc = 1;           // LBC_OPT_TEAM_WG_PER_CU
     int team_size = 0;          // LBC_OPT_TEAM_SIZE (0: CUs / 8)
+    int team_ll_max = 0;        // the recorded team program: most weight fragments of one item's K slice (fast path)
+    int team_ring_last = 0;     // ring slots per K slice of the last team launch (0: no weight ring)
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -1439,9 +1441,13 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
     a.ni_max = 2;
     a.tab16 = rans[0].total16;
+    m0->team_ll_max = 0;
     for (const GemmArgs& d : gem) {
         const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
-        if (team_fast_path(d, S)) a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
+        if (!team_fast_path(d, S)) continue;
+        a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
+        const int nkb = d.K >> 4;
+        m0->team_ll_max = std::max(m0->team_ll_max, nkb / KSPLIT + (nkb % KSPLIT ? 1 : 0));
     }
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
     // before it run beside the rANS decode when every workgroup takes the fast path for it
@@ -1540,9 +1546,12 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory
         a.dense = sparse ? 0 : 1;
+        // the weight ring (team.hip): whatever LDS one workgroup per CU leaves, unless LBIC_TEAM_RING=0 (A/B runs)
+        const char* rge = getenv("LBIC_TEAM_RING");
+        a.ring_q = (rge && atoi(rge) == 0) || wpc > 1 ? 0 : team_ring_slots(a, m0->team_ll_max, 160 * 1024);
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
-        const int nb = team_blocks_per_cu(a.dense, lds);
+        const int nb = team_blocks_per_cu(a.dense, a.ring_q > 0, lds);
         if (nb >= wpc) break;
         if (nb < 1 || wpc == 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         wpc = nb;
@@ -1597,6 +1606,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     if (fail)   // any other failure word is a protocol error, not a residency problem: report it
         return set_error(LBC_E_STATE, "team decode: unexpected failure word " + std::to_string(fail));
     m0->team_plain_last = a.plain;
+    m0->team_ring_last = a.ring_q;
     m0->team_mode_last = a.dense == 1 ? 2 : 1;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
@@ -1624,6 +1634,12 @@ int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double*
     *bytes = m->team_launch_bytes;
     *flops = m->team_launch_flops;
     *plain = m->team_plain_last;
+    return LBC_OK;
+}
+
+int lbc_team_ring(const lbc_model* m, int* slots) {
+    if (!m || !slots) return set_error(LBC_E_ARG, "null argument");
+    *slots = m->team_ring_last;
     return LBC_OK;
 }
 

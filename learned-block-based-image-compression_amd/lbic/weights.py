@@ -51,6 +51,11 @@ MID_POINTS = {   # (B, N, M) -> (latent gain, scale level); calibration bpp on a
     (4, 512, 96): (0.6767, 0.2508),     # B4_highrate: 1.570 bpp (published 1.58)
 }
 MID_DEFAULT = (1.0, 0.3)
+# rate="low" latent gain per architecture (default LOW_Y_GAIN): B16_lowrate's published point is 0.120 bpp, which the
+# default gain undershoots (0.07 bpp on noise frames); calibrated by tests/golden/tune_mid_rate.py (LOW_TARGETS)
+LOW_POINTS = {   # (B, N, M) -> latent gain; calibration bpp on a noise frame
+    (16, 1280, 192): 0.4905,    # B16_lowrate: 0.1211 bpp on a 128x128 noise frame (published 0.120)
+}
 
 
 def mid_point(arch: Arch):
@@ -65,13 +70,14 @@ def rate_for_lambda(lam: float) -> str:
 
 
 def synth_state_dict(arch: Arch, seed: int = 1337, rate: str = "high", mid=None) -> Dict[str, np.ndarray]:
-    """mid: (latent gain, scale level) overriding mid_point(arch) for rate="mid" (calibration only)."""
+    """mid: (latent gain, scale level) overriding mid_point(arch) for rate="mid", or (latent gain, -) overriding
+    LOW_POINTS for rate="low" (calibration only)."""
     if rate not in ("high", "low", "mid"):
         raise ValueError(f"rate must be 'high', 'mid' or 'low', not {rate!r}")
     low = rate in ("low", "mid")
     y_gain_low, s_mid = mid if mid is not None else mid_point(arch)
     if rate == "low":
-        y_gain_low = LOW_Y_GAIN
+        y_gain_low = mid[0] if mid is not None else LOW_POINTS.get((arch.B, arch.N, arch.M), LOW_Y_GAIN)
     rng = np.random.default_rng(seed)
     out: Dict[str, np.ndarray] = {}
     convs = {c[0]: c for c in arch.conv_specs()}

@@ -27,6 +27,11 @@ def golden_arch(g):
     return Arch(int(g["B"]), tuple(int(k) for k in g["KS"]), int(g["N"]), int(g["M"]))
 
 
+def golden_rate(g):
+    """The synthetic-weight operating point a fixture was generated at (lbic.weights.synth_state_dict rate)."""
+    return str(g["rate"]) if "rate" in g else "high"
+
+
 @pytest.fixture(scope="session")
 def golden():
     return load_golden

@@ -42,7 +42,7 @@ from lbic.weights import synth_state_dict  # noqa: E402
 TIE_EPS = 1e-5
 WEIGHT_SEED = 1337
 
-# name -> (arch, H, W, first image seed)
+# name -> (arch, H, W, first image seed[, weight operating point (lbic.weights.synth_state_dict rate; default "high")])
 LOOPS = {
     "tiny_ks3111": (Arch(4, (3, 1, 1, 1), 64, 16), 32, 32, 100),
     "tiny_ks3311": (Arch(4, (3, 3, 1, 1), 64, 16), 32, 32, 200),
@@ -50,6 +50,11 @@ LOOPS = {
     "b8_highrate": (Arch(8, (3, 3, 1, 1), 1152, 128), 48, 48, 400),
     "b4_highrate": (Arch(4, (3, 3, 1, 1), 512, 96), 32, 32, 500),
     "b16_lowrate": (Arch(16, (3, 1, 1, 1), 1280, 192), 48, 48, 600),
+    # the operating points bench.py times configs 3-4 at (rate="mid", ~1.6 bpp: the configs' published points)
+    "b8_highrate_mid": (Arch(8, (3, 3, 1, 1), 1152, 128), 48, 48, 410, "mid"),
+    "b4_highrate_mid": (Arch(4, (3, 3, 1, 1), 512, 96), 32, 32, 510, "mid"),
+    # config 5's operating point (rate="low", calibrated per architecture: ~0.12 bpp, the config's published point)
+    "b16_lowrate_low": (Arch(16, (3, 1, 1, 1), 1280, 192), 48, 48, 610, "low"),
 }
 
 
@@ -110,8 +115,8 @@ def gen_cdf(out):
     print("cdf_pmf:", len(pmfs), "tables, total", lens.sum())
 
 
-def gen_loop(name, arch, H, W, seed0, stages_out=None):
-    sd = synth_state_dict(arch, WEIGHT_SEED)
+def gen_loop(name, arch, H, W, seed0, rate="high", stages_out=None):
+    sd = synth_state_dict(arch, WEIGHT_SEED, rate=rate)
     model, net = refshim.make_model(arch, sd)
     model.update(force=True)
     table = net.get_scale_table().numpy()
@@ -147,7 +152,7 @@ def gen_loop(name, arch, H, W, seed0, stages_out=None):
     xb = x[0].permute(1, 2, 0).contiguous().numpy()
     np.savez_compressed(
         os.path.join(HERE, f"loop_{name}.npz"),
-        B=arch.B, KS=np.array(arch.KS), N=arch.N, M=arch.M, weight_seed=WEIGHT_SEED, image_seed=seed,
+        B=arch.B, KS=np.array(arch.KS), N=arch.N, M=arch.M, weight_seed=WEIGHT_SEED, image_seed=seed, rate=rate,
         image=img[0], x=xb, symbols=syms, indexes=idxs,
         zhat=zhat[0].permute(1, 2, 0).contiguous().numpy(),
         zhat_dec=zdec[0].permute(1, 2, 0).contiguous().numpy(),
@@ -389,8 +394,8 @@ if __name__ == "__main__":
         if only and ("forward_" + name) not in only:
             continue
         gen_forward(name, arch, H, W, s0)
-    for name, (arch, H, W, s0) in LOOPS.items():
+    for name, (arch, H, W, s0, *rate) in LOOPS.items():
         if only and name not in only:
             continue
-        gen_loop(name, arch, H, W, s0,
+        gen_loop(name, arch, H, W, s0, rate=(rate or ["high"])[0],
                  stages_out=os.path.join(HERE, "stages_b8_lowrate.npz") if name == "b8_lowrate_2rows" else None)

@@ -28,10 +28,13 @@ TARGETS = {   # arch -> published bpp
     Arch(4, (3, 3, 1, 1), 512, 96): 1.58,
 }
 SIZE = 64
+LOW_TARGETS = {   # rate="low": arch -> published bpp (B16_lowrate: 0.1200); frame size
+    Arch(16, (3, 1, 1, 1), 1280, 192): (0.120, 128),
+}
 
 
-def code(arch, g, s, xb):
-    ref = TorchRef(arch, synth_state_dict(arch, 1337, rate="mid", mid=(g, s)))
+def code(arch, g, s, xb, rate="mid"):
+    ref = TorchRef(arch, synth_state_dict(arch, 1337, rate=rate, mid=(g, s)))
     out = ref.compress(xb)
     bpp = len(out["bytes"]) * 8.0 / (xb.shape[0] * xb.shape[1] * arch.B * arch.B)
     return bpp, out
@@ -39,6 +42,21 @@ def code(arch, g, s, xb):
 
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for arch, (target, size) in LOW_TARGETS.items():
+        img = np.random.default_rng(0).integers(0, 256, (3, size, size), dtype=np.uint8).astype(np.float32) / 255 - 0.5
+        xb = O.image_to_blocks(img, arch.B)
+        lo, hi = math.log(0.05), math.log(20.0)
+        for it in range(12):
+            g = math.exp(0.5 * (lo + hi))
+            bpp, _ = code(arch, g, 0.0, xb, rate="low")
+            print(f"{arch} low: g={g:.4f} -> {bpp:.4f} bpp (target {target})", flush=True)
+            if bpp > target:
+                hi = math.log(g)
+            else:
+                lo = math.log(g)
+        print(f"LOW_POINTS[({arch.B}, {arch.N}, {arch.M})] = {g:.4f}  # {bpp:.4f} bpp on {size}x{size} noise")
+    if "low" in sys.argv[1:]:
+        return
     for arch, target in TARGETS.items():
         img = np.random.default_rng(0).integers(0, 256, (3, SIZE, SIZE), dtype=np.uint8).astype(np.float32) / 255 - 0.5
         xb = O.image_to_blocks(img, arch.B)

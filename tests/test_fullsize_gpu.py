@@ -118,12 +118,15 @@ FULL = {   # BASELINE.json configs 3-5 at their frame sizes (one frame on one GP
 }
 
 
-@pytest.mark.parametrize("name", sorted(FULL))
-def test_config_full_size_roundtrip(name):
+# rate: the weights' operating point -- "high" (12-47 bpp, every symbol busy) and the configs' own points that
+# bench.py times: "mid" (~1.6 bpp) for the high-rate configs, "low" (~0.12 bpp) for B16_lowrate
+@pytest.mark.parametrize("name,rate", [("B8_highrate", "high"), ("B8_highrate", "mid"), ("B4_highrate", "high"),
+                                       ("B4_highrate", "mid"), ("B16_lowrate", "low")])
+def test_config_full_size_roundtrip(name, rate):
     from lbic.arch import Arch
     (B, KS, N, M), H, W = FULL[name]
     arch = Arch(B, KS, N, M)
-    sd = synth_state_dict(arch, 1337, rate="low" if "lowrate" in name else "high")
+    sd = synth_state_dict(arch, 1337, rate=rate)
     m = _model(arch, sd)
     img = np.random.default_rng(42).integers(0, 256, (3, H, W)).astype(np.float32) / 255 - 0.5
     xb = O.image_to_blocks(img, B)
@@ -132,7 +135,9 @@ def test_config_full_size_roundtrip(name):
     Hb, Wb = xb.shape[:2]
     z = m.decompress_batch(streams, Hb, Wb)
     assert torch.equal(z, r["zhat"]), "decode != encode at full size"
-    print(f"{name} {H}x{W}: {len(streams[0]) * 8 / (H * W):.4f} bpp")
+    bps = 8.0 * len(streams[0]) / (Hb * Wb * M)
+    print(f"{name} {H}x{W} rate {rate}: {len(streams[0]) * 8 / (H * W):.4f} bpp, {bps:.3f} bits/symbol "
+          f"({'sparse' if bps < 1.0 else 'dense'} rANS)")
     blocks = [(0, 0), (0, Wb - 1), (1, 1), (Hb // 2, Wb // 3), (Hb - 1, 0), (Hb - 1, Wb - 1)]
     _teacher_forced(arch, sd, xb, r["zhat"][0].cpu().numpy(), r["symbols"][0].cpu().numpy(),
                     r["indexes"][0].cpu().numpy(), blocks)
@@ -168,6 +173,9 @@ TEAM_FULL = {   # (arch, H, W, batches, frames per batch, rate): every config's 
     "B8_highrate": ((8, (3, 3, 1, 1), 1152, 128), 512, 768, 3, 3, "high"),
     "B4_highrate": ((4, (3, 3, 1, 1), 512, 96), 768, 768, 2, 2, "high"),
     "B16_lowrate": ((16, (3, 1, 1, 1), 1280, 192), 2048, 2048, 2, 2, "low"),
+    # the operating points bench.py times configs 3-4 at (rate="mid"): the Kodak-24 shard per GPU of 8, B4 batches
+    "B8_highrate_mid": ((8, (3, 3, 1, 1), 1152, 128), 512, 768, 3, 3, "mid"),
+    "B4_highrate_mid": ((4, (3, 3, 1, 1), 512, 96), 768, 768, 2, 4, "mid"),
 }
 
 
@@ -198,7 +206,7 @@ def test_team_full_size_roundtrip(name):
         assert torch.equal(got[t], zs[t]), f"{name} batch {t}: {(got[t] != zs[t]).sum().item()} values differ"
     bps = 8.0 * nbytes / (T * n * Hb * Wb * M)
     mode = hs[0].team_stats()["mode"]
-    print(f"{name} {T} x {n} x {H}x{W}: {bps:.3f} bits per symbol, {mode}")
+    print(f"{name} {T} x {n} x {H}x{W}: {bps:.3f} bits per symbol, {mode}, ring {hs[0].team_stats()['ring_slots']}")
     assert mode == ("team_sparse" if bps < 1.0 else "team_dense")
 
 

@@ -8,23 +8,24 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_rel, golden_arch, load_golden
+from conftest import assert_rel, golden_arch, golden_rate, load_golden
 from lbic.weights import synth_state_dict
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows"]
+LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows",
+         "b8_highrate_mid", "b4_highrate_mid", "b16_lowrate_low"]
 _MODELS = {}
 
 
-def model_for(arch, seed=1337):
+def model_for(arch, seed=1337, rate="high"):
     from lbic.model import BlockBasedImgCompLossyNetv9
-    key = (arch, seed)
+    key = (arch, seed, rate)
     if key not in _MODELS:
         cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
         m = BlockBasedImgCompLossyNetv9(cfg)
-        m.load_state_dict(synth_state_dict(arch, seed))
+        m.load_state_dict(synth_state_dict(arch, seed, rate=rate))
         m.update(force=True)
         _MODELS[key] = m
     return _MODELS[key]
@@ -39,7 +40,7 @@ def tables():
 def test_closed_loop_matches_reference(name, tables):
     g = load_golden("loop_" + name)
     arch = golden_arch(g)
-    m = model_for(arch, int(g["weight_seed"]))
+    m = model_for(arch, int(g["weight_seed"]), golden_rate(g))
     x = torch.from_numpy(g["x"])[None].cuda()
     r = m.compress_batch(x, want_bits=True)
     sym = r["symbols"][0].cpu().numpy()
@@ -52,6 +53,10 @@ def test_closed_loop_matches_reference(name, tables):
     assert streams[0] == tables.encode(g["symbols"], g["indexes"])
     zdec = m.decompress_batch(streams, *g["x"].shape[:2])
     assert torch.equal(zdec, r["zhat"]), "decoder reconstruction differs from the encoder's"
+    assert_rel(zdec.cpu().numpy()[0], g["zhat_dec"], what="decoded zhat vs the reference's decompress()")
+    bps = 8.0 * len(streams[0]) / sym.size
+    print(f"{name} ({golden_rate(g)}): {bps:.3f} bits/symbol, rANS variant "
+          f"{'sparse' if bps < 1.0 else 'dense'}, max |zhat - ref| {np.abs(z - g['zhat']).max():.2e}")
 
 
 def test_bits_match_oracle_likelihood():

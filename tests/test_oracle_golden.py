@@ -6,7 +6,7 @@ tie-screened fixtures (tests/golden/gen_golden.py), scale table and pmfs bit-exa
 import numpy as np
 import pytest
 
-from conftest import golden_arch, load_golden
+from conftest import golden_arch, load_golden, golden_rate
 from lbic.weights import synth_state_dict
 from oracle import oracle as O
 
@@ -94,7 +94,8 @@ def test_stages_b8_lowrate():
         assert _close(bits, g["bits"][bi]) < 1e-4
 
 
-LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows"]
+LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows",
+         "b8_highrate_mid", "b4_highrate_mid", "b16_lowrate_low"]
 
 
 @pytest.mark.parametrize("name", LOOPS)
@@ -103,7 +104,7 @@ def test_closed_loop_matches_reference(name):
     reconstruction within 1e-5; decompress() of our own bitstream reproduces the reference decoder."""
     g = load_golden("loop_" + name)
     arch = golden_arch(g)
-    codec = O.OracleCodec(arch, synth_state_dict(arch, int(g["weight_seed"])))
+    codec = O.OracleCodec(arch, synth_state_dict(arch, int(g["weight_seed"]), rate=golden_rate(g)))
     out = codec.compress(g["x"])
     assert np.array_equal(out["indexes"], g["indexes"])
     assert np.array_equal(out["symbols"], g["symbols"])

@@ -22,13 +22,14 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_rel, golden_arch, load_golden
+from conftest import assert_rel, golden_arch, golden_rate, load_golden
 from lbic.weights import synth_state_dict
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows"]
+LOOPS = ["tiny_ks3111", "tiny_ks3311", "b4_highrate", "b16_lowrate", "b8_highrate", "b8_lowrate_2rows",
+         "b8_highrate_mid", "b4_highrate_mid", "b16_lowrate_low"]
 _H = {}
 
 
@@ -59,7 +60,7 @@ def test_team_decodes_reference_stream(name, sparse, spread, monkeypatch):
     Hb, Wb = g["x"].shape[:2]
     stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
     T, n = 3, 2
-    hs = _handles(arch, int(g["weight_seed"]), "high", T)
+    hs = _handles(arch, int(g["weight_seed"]), golden_rate(g), T)
     got = decompress_teams(hs, [[stream] * n for _ in range(T)], Hb, Wb)
     st = hs[0].team_stats()
     assert st["mode"] == ("team_sparse" if sparse == "1" else "team_dense"), st
