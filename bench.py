@@ -7,19 +7,16 @@ the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-59
 compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
 rANS decode).  Every decode pass decodes exactly one 32-frame batch (32 frames in flight per pass).
 
-Schedule of the headline (`value`): `--workers` (default 4) workers, each a codec handle on the shared weights
-(lbc_create_sibling) with its own HIP stream and host thread, take the `--steps` batches in turn and compress,
-entropy code and decode each whole batch; so up to four 32-frame decode passes run side by side with the other
-workers' encodes, and a worker's host rANS of batch k overlaps its stream's compress of its next batch.  Four,
-because dependent kernel chains overlap on at most four busy hardware queues; every stream gets a
-queue of its own (lbic/streams.py; GPU_MAX_HW_QUEUES = --hw-queues).
-`--workers 0` selects the encoder + `--depth` decoders pipeline instead (one encoder handle compresses batch k+1
-while the decoder handles decode earlier batches).  The timed region holds exactly the `--steps` compressions
-and the `--steps` decompressions of the same batches, fill and drain included; inputs are resident in HBM when
-it starts.  Reported beside it: one decode pass in flight (`one_decode_in_flight`), no overlap at all
-(`serial_schedule`), the gang schedule (`gang_schedule`: one raster pass over several queued batches, more
-frames in flight, not the headline), and the opt-in sub-stream format (`substream_format`, not the reference
-bitstream).
+Schedule of the headline (`value`, `--team 8`, the default): one encoder handle compresses batch after batch on its
+own HIP stream (host rANS on helper threads); every 8 encoded batches are decoded by ONE persistent k_dec_team launch
+(lbc_decode_team: one team of workgroups per 32-frame batch, team barriers instead of kernel boundaries) on a second
+stream, beside the encoder's next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
+shared weights, each compressing, entropy coding and decoding whole batches) or, with `--workers 0`, the encoder +
+`--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
+decompressions of the same batches, fill and drain included; inputs are resident in HBM when it starts.  Reported
+beside it: one decode pass in flight (`one_decode_in_flight`), no overlap at all (`serial_schedule`), the gang
+schedule (`gang_schedule`: one raster pass over several queued batches, more frames in flight, not the headline),
+and the opt-in sub-stream format (`substream_format`, not the reference bitstream).
 
 Weights: the seeded synthetic set (lbic.weights) at the config's operating point (`--rate low`: about
 0.13 bpp on these frames, BASELINE.md's B8_lowrate point is 0.117 bpp); `--rate high` is the 12 bpp set.
@@ -104,6 +101,9 @@ def parse_args(argv=None):
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts, unless already in the environment): "
                          "every busy stream needs a hardware queue of its own (lbic/streams.py)")
     ap.add_argument("--sample-every", type=int, default=16, help="kernel timing-stamp sampling period (steps)")
+    ap.add_argument("--enc-sample-every", type=int, default=16,
+                    help="team schedule: in-kernel timing stamps in every n-th wavefront step of the encoder graph (the "
+                         "k_gemm launch duration of the bench line; 0 = none: graph wall time / launches only)")
     ap.add_argument("--cpu-budget", type=float, default=24.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--side-steps", type=int, default=2,
                     help="batches of the one-decode-in-flight and serial schedules reported beside (0 = skip)")
@@ -560,10 +560,10 @@ def main():
         return dict(value=round(world * n * H * W / (dt / k) / 1e6, 4), ms_per_step=round(dt / k * 1e3, 2),
                     steps=k, phases_ms_per_step={kk: round(v / k * 1e3, 2) for kk, v in ph.items()}, **extra)
 
-    # sampling is part of the captured graphs: enable it before the first capture.  The team schedule samples nothing:
-    # its decode is one persistent launch (HIP events) and the encoder graph is timed by HIP events too (in-kernel
-    # stamps on the encoder's 1,500-workgroup launches would themselves slow the sampled launches)
-    sample_every = 0 if args.team else args.sample_every
+    # sampling is part of the captured graphs: enable it before the first capture.  The team schedule: its decode is
+    # one persistent launch (HIP events); the encoder graph is timed by HIP events AND every --enc-sample-every-th
+    # wavefront step's launches carry in-kernel stamps (a launch's own duration: the graph's two branches overlap)
+    sample_every = args.enc_sample_every if args.team else args.sample_every
     for m_ in handles:
         m_.profile_begin(sample_every)
     if args.encode_only:      # e.g. rocprofv3 --pmc on the encoder's launch shapes
@@ -728,16 +728,36 @@ def roofline(kstats, dt, team=None, enc=None):
     work of all launches (lbc_kernel_stat.total_flops / total_bytes)."""
     kernels, fam = {}, {}
     if enc is not None and kstats:
+        # the encoder graph forks every wavefront step into two branches that run concurrently, so graph time / launches
+        # (`wall_us_per_launch`) is not a launch's duration.  A launch's duration (what a dispatch trace such as rocprofv3
+        # --kernel-trace reports) comes from the in-kernel stamps of the sampled k_gemm launches: earliest workgroup
+        # start to latest workgroup end on the 100 MHz constant clock (lbc_profile_begin(sample_every))
         n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
+        sg = kstats.get("k_gemm", {})
         if n_all and enc["ms"] > 0:
-            per = enc["ms"] / n_all
+            wall = enc["ms"] / n_all
             tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
             tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
-            kernels["k_gemm"] = dict(launches_sampled=0, launches_total=int(n_all), avg_span_us=round(per * 1e3, 3),
-                                     avg_launch_us=round(per * 1e3, 3), est_share_of_step=round(enc["ms"] / 1e3 / dt, 4),
-                                     timing=f"HIP events around {enc['passes']} encoder graphs / their launches "
-                                            "(k_gemm + k_gemm_s ramp steps)")
-            fam["k_gemm"] = (tf / n_all, tb / n_all)
+            if sg.get("launches"):
+                per = sg["total_ms"] / sg["launches"]
+                n_k = int(sg["total_launches"])
+                kernels["k_gemm"] = dict(launches_sampled=int(sg["launches"]), launches_total=n_k,
+                                         avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
+                                         wall_us_per_launch=round(wall * 1e3, 3),
+                                         est_share_of_step=round(per * n_k / 1e3 / dt, 4),
+                                         timing="in-kernel stamps of the sampled k_gemm launches (earliest workgroup "
+                                                "start -> latest end; the forked branches overlap, so the summed "
+                                                f"durations exceed the encoder's wall time, {enc['ms'] / 1e3:.3f} s "
+                                                f"over {enc['passes']} encoder graphs)")
+                fam["k_gemm"] = (sg["flops"] / sg["launches"], sg["bytes"] / sg["launches"])
+            else:
+                kernels["k_gemm"] = dict(launches_sampled=0, launches_total=int(n_all), avg_span_us=round(wall * 1e3, 3),
+                                         avg_launch_us=round(wall * 1e3, 3), wall_us_per_launch=round(wall * 1e3, 3),
+                                         est_share_of_step=round(enc["ms"] / 1e3 / dt, 4),
+                                         timing=f"HIP events around {enc['passes']} encoder graphs / their launches "
+                                                "(k_gemm + k_gemm_s ramp steps; the forked branches overlap, so this "
+                                                "understates a launch's own duration)")
+                fam["k_gemm"] = (tf / n_all, tb / n_all)
         kstats = {}
     for name, s in (kstats or {}).items():
         span = s["total_ms"] / max(s["launches"], 1)
@@ -760,17 +780,30 @@ def roofline(kstats, dt, team=None, enc=None):
         fam["k_dec_team"] = (team["flops"] / team["launches"], team["bytes"] / team["launches"])
     if not kernels:
         return None, {}
+    # dominant = the most summed launch duration in the timed region (a dispatch trace's "total duration"); with the
+    # encoder's forked branches and the team decoder running concurrently the summed durations exceed the region
     dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_total"])
     if not fam[dom][1]:
         return None, kernels
-    per_launch_s = kernels[dom]["avg_launch_us"] * 1e-6
+    ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+
+    def bound_of(name):
+        fl_, by_ = fam[name]
+        s_ = kernels[name]["avg_launch_us"] * 1e-6
+        if fl_ > 0 and by_ and fl_ / by_ >= ridge:
+            return fl_ / s_ / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
+        return by_ / s_ / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    per_kernel = {}
+    for name in kernels:
+        if name in fam and fam[name][1]:
+            a_, p_, u_, b_ = bound_of(name)
+            per_kernel[name] = dict(bound=b_, achieved=round(a_, 4), peak=p_, unit=u_, frac=round(a_ / p_, 5),
+                                    avg_launch_us=kernels[name]["avg_launch_us"],
+                                    summed_duration_s=round(kernels[name]["avg_launch_us"] *
+                                                            kernels[name]["launches_total"] * 1e-6, 4))
     fl, by = fam[dom]
     ai = fl / by if by else float("inf")
-    ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
-    if fl > 0 and ai >= ridge:
-        ach, peak, unit, bound = fl / per_launch_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
-    else:
-        ach, peak, unit, bound = by / per_launch_s / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    ach, peak, unit, bound = bound_of(dom)
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/gpu_profile.sh, tools/team_pmc.sh)
@@ -785,7 +818,10 @@ def roofline(kstats, dt, team=None, enc=None):
                 traffic=traffic, avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],
                 algorithmic_per_launch=dict(flops=round(fl), bytes=round(by)), arithmetic_intensity=round(ai, 2),
                 frac_of_span=round((fl / (kernels[dom]["avg_span_us"] * 1e-6) / 1e12 / peak) if bound == "mfma" else
-                                   (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5))
+                                   (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5),
+                per_kernel=per_kernel,
+                dominant_rule="largest summed launch duration in the timed region (avg launch duration x launches); "
+                              "concurrent kernels' summed durations may exceed the region")
     return roof, kernels
 
 

@@ -1536,9 +1536,14 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         S = std::min(32, cus / TEAM_MAX) * wpc;
         if (m0->team_size > 0) S = std::min(S, m0->team_size * wpc);
         // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
-        // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=1 keeps one XCD
+        // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=P (1, 2, 4, 8 with
+        // T <= 8 / P) sets the XCD slots per team (A/B runs)
         const char* spe = getenv("LBIC_TEAM_SPREAD");
-        spread = T <= TEAM_MAX / 2 && !(spe && atoi(spe) == 1) ? 2 : 1;
+        spread = T <= TEAM_MAX / 2 ? 2 : 1;
+        if (spe) {
+            const int p = atoi(spe);
+            if ((p == 1 || p == 2 || p == 4 || p == 8) && T <= TEAM_MAX / p) spread = p;
+        }
         S *= spread;
         if (S < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse))) return rc;
@@ -1546,9 +1551,10 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory
         a.dense = sparse ? 0 : 1;
-        // the weight ring (team.hip): whatever LDS one workgroup per CU leaves, unless LBIC_TEAM_RING=0 (A/B runs)
+        // the weight ring (team.hip), opt-in (LBIC_TEAM_RING=1): whatever LDS one workgroup per CU leaves.  Measured
+        // slower than the register-prefetch path, so not the default
         const char* rge = getenv("LBIC_TEAM_RING");
-        a.ring_q = (rge && atoi(rge) == 0) || wpc > 1 ? 0 : team_ring_slots(a, m0->team_ll_max, 160 * 1024);
+        a.ring_q = !(rge && atoi(rge) == 1) || wpc > 1 ? 0 : team_ring_slots(a, m0->team_ll_max, 160 * 1024);
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         const int nb = team_blocks_per_cu(a.dense, a.ring_q > 0, lds);
@@ -1577,7 +1583,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     // spread over XCDs stops before its first operation (failure word 2, nothing decoded yet) and is rerun with
     // write-through hand-offs
     const char* sc1e = getenv("LBIC_TEAM_SC1");
-    a.plain = (sc1e && atoi(sc1e)) || a.spread == 2 ? 0 : 1;
+    a.plain = (sc1e && atoi(sc1e)) || a.spread > 1 ? 0 : 1;
     unsigned fail = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if ((rc = reset())) return rc;
@@ -1832,12 +1838,16 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
         };
         for (const auto& r : p.recs) {
             const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;
+            // the launch's span: earliest workgroup start over the XCDs -> latest workgroup end over the XCDs (what a
+            // dispatch trace measures; the XCDs do not start a launch at the same moment)
             long long span = -1;
+            unsigned long long s0 = ~0ull, e1 = 0;
             for (int x = 0; x < 8; ++x) {
                 if (!t[2 * x] || !t[2 * x + 1]) continue;
-                const long long d = (long long)(t[2 * x + 1] - (~0ull - t[2 * x]));
-                if (d >= 0 && d > span) span = d;
+                s0 = std::min(s0, ~0ull - t[2 * x]);
+                e1 = std::max(e1, t[2 * x + 1]);
             }
+            if (e1 && e1 >= s0) span = (long long)(e1 - s0);
             if (span >= 0 && r.prev >= 0) {    // launch-to-launch period in the stream chain
                 const unsigned long long e0 = last_end(r.prev), e1 = last_end(r.slot);
                 if (e0 && e1 > e0 && e1 - e0 < 100000000ull) {

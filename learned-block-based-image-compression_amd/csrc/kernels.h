@@ -129,8 +129,8 @@ struct TeamArgs {
                              // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>
                              // on them; 0: rans_row_sparse (centre intervals, tables from global memory)
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
-    int spread;              // XCD slots per team: 1, or 2 (T <= 4: team t = the workgroups on slots 2t and 2t + 1, S
-                             // ranks over two XCDs; hand-offs write-through, plain = 0)
+    int spread;              // XCD slots per team P: 1, 2, 4 or 8 (T <= 8 / P: team t = the workgroups on slots P t ..
+                             // P t + P - 1, S ranks over P XCDs; P > 1: hand-offs write-through, plain = 0)
     int ring_q;              // > 0: the weight-ring instance (team.hip): loader waves stream every fast-path GEMM's
                              // weights into 8 LDS rings of ring_q 1-KB slots; 0: the computing waves load them
 };

@@ -543,10 +543,11 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
-    // spread 2 (at most four teams): team t = the workgroups of slots 2t and 2t + 1 (two XCDs), ranks interleaved
+    // spread P = 2, 4, 8 (at most 8 / P teams): team t = the workgroups of slots P t .. P t + P - 1 (P XCDs), ranks
+    // interleaved over them
     const int slot = blockIdx.x & 7;
-    const int team = ta.spread == 2 ? slot >> 1 : slot;
-    const int rank = ta.spread == 2 ? (int)(((blockIdx.x >> 3) << 1) | (slot & 1)) : (int)(blockIdx.x >> 3);
+    const int team = slot / ta.spread;
+    const int rank = (int)(blockIdx.x >> 3) * ta.spread + slot % ta.spread;
     if (team >= T || rank >= S) return;
     unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
@@ -688,7 +689,8 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     (void)attr;
     const size_t lds = team_lds_bytes(a);
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
-    if (a.spread != 1 && (a.spread != 2 || a.T > TEAM_MAX / 2 || a.S % 2 || a.plain))
+    if ((a.spread != 1 && a.spread != 2 && a.spread != 4 && a.spread != 8) ||
+        (a.spread > 1 && (a.T > TEAM_MAX / a.spread || a.S % a.spread || a.plain)))
         return set_error(LBC_E_ARG, "bad team spread");
     const dim3 grid(8 * a.S / a.spread);
     if (a.dense) hipLaunchKernelGGL((k_dec_team<true, false>), grid, dim3(512), lds, s, a);

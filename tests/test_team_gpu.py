@@ -63,7 +63,7 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
 ])
 def test_team_equals_graph_decoder(name, T, n, shape, ring, monkeypatch):
     """Image counts of one, two, three and four row tiles, 1-8 teams; the weights streamed through the LDS rings by
-    loader waves (ring "1", the default) or loaded by the computing waves (LBIC_TEAM_RING=0)."""
+    loader waves (ring "1", LBIC_TEAM_RING=1, opt-in) or loaded by the computing waves (the default)."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
     monkeypatch.setenv("LBIC_TEAM_RING", ring)
     g = load_golden("loop_" + name)
