@@ -106,6 +106,13 @@ struct Prof {
     long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
     double work_replay[8][4][2] = {};      // their algorithmic FLOPs and bytes per replay (every launch, sampled or not)
     long long replays[8] = {};             // replays of each range's graph since lbc_profile_begin
+    bool nochain = false;                  // capturing a forked graph: no launch-to-launch period (two chains)
+    // the encoder graph's slot range (0) copied to the host after EVERY replay since lbc_profile_begin (its stamps are
+    // zeroed at the head of each replay): lbc_profile_end averages over all of them, not only the last replay
+    int used0 = 0;                         // slots of range 0 the captured encoder graph uses
+    unsigned long long* snap = nullptr;    // pinned host ring: kSnaps x kSlotsPerRange x kSlotU64 words
+    int nsnap = 0;
+    static constexpr int kSnaps = 64;
     unsigned long long* take() {
         if (!slots || next >= kSlotsPerRange) return nullptr;
         return slots + kSlotU64 * ((size_t)range * kSlotsPerRange + next++);
@@ -116,7 +123,7 @@ struct Prof {
     }
     void add(int cls, const unsigned long long* ts, double flops, double bytes) {
         const int slot = (int)((ts - slots) / kSlotU64);
-        recs.push_back({cls, slot, flops, bytes, last_slot});
+        recs.push_back({cls, slot, flops, bytes, nochain ? -1 : last_slot});
         last_slot = slot;
     }
 };
@@ -860,6 +867,7 @@ void lbc_destroy(lbc_model* m) {
     for (auto& st : m->lstream)
         if (st) (void)hipStreamDestroy(st);
     if (m->prof.slots) (void)hipFree(m->prof.slots);
+    if (m->prof.snap) (void)hipHostFree(m->prof.snap);
     if (m->enc_exec) (void)hipGraphExecDestroy(m->enc_exec);
     if (m->wf_exec) (void)hipGraphExecDestroy(m->wf_exec);
     for (auto e : m->dec_exec) (void)hipGraphExecDestroy(e);
@@ -999,8 +1007,9 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         int crc = prof_range_begin(&m->prof, 0, m->cap);
         drop_recs(m->prof, 0);
         const int4* blocks = m->blocks_enc.as<int4>();
-        const bool fork = enc_fork_on() && m->prof.sample_every == 0;   // (timing stamps assume one chain)
+        const bool fork = enc_fork_on();   // (sampled: launch spans only, no launch-to-launch period)
         g_prof = &m->prof;
+        m->prof.nochain = fork;
         for (size_t t = 0; t < m->step_off.size(); ++t)
             if (m->step_cnt[t] > m->lane[0].rows) crc = set_error(LBC_E_STATE, "encoder workspace too small");
         for (size_t t = 0; t < m->step_off.size() && !crc; ++t) {
@@ -1026,6 +1035,8 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
             if (!crc) crc = run_dec(m, m->lane[0], g, m->cap);
         }
         m->prof.active = false;
+        m->prof.nochain = false;
+        m->prof.used0 = m->prof.next;
         g_prof = nullptr;
         hipGraph_t graph = nullptr;
         const hipError_t e = hipStreamEndCapture(m->cap, &graph);
@@ -1044,6 +1055,12 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         return rc;
     HIPCHK(hipGraphLaunch(m->enc_exec, s));
     m->prof.replays[0] += 1;
+    if (m->prof.sample_every && m->prof.slots && m->prof.snap && m->prof.used0 > 0 && m->prof.nsnap < Prof::kSnaps) {
+        // this replay's stamps, before the next replay zeroes them (stream order)
+        HIPCHK(hipMemcpyAsync(m->prof.snap + (size_t)m->prof.nsnap * kSlotsPerRange * kSlotU64, m->prof.slots,
+                              (size_t)m->prof.used0 * kSlotU64 * 8, hipMemcpyDeviceToHost, s));
+        m->prof.nsnap += 1;
+    }
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipMemcpyAsync(sym_dev, m->sym_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(idx_dev, m->idx_buf.p, nsym * 4, hipMemcpyDeviceToDevice, s));
@@ -1768,6 +1785,8 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
             if (!crc) crc = run_dec(m, w, g, m->cap);
         }
         m->prof.active = false;
+        m->prof.nochain = false;
+        m->prof.used0 = m->prof.next;
         g_prof = nullptr;
         hipGraph_t graph = nullptr;
         const hipError_t e = hipStreamEndCapture(m->cap, &graph);
@@ -1807,6 +1826,9 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
     if (sample_every != p.sample_every) p.recs.clear();
     p.sample_every = sample_every;
     for (auto& r : p.replays) r = 0;
+    if (sample_every && !p.snap)
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p.snap), (size_t)Prof::kSnaps * kSlotsPerRange * kSlotU64 * 8));
+    p.nsnap = 0;
     if (p.slots) {
         HIPCHK(hipSetDevice(m->cfg.device));
         HIPCHK(hipDeviceSynchronize());
@@ -1836,18 +1858,32 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
                 if (t[2 * x] && t[2 * x + 1]) e = std::max(e, t[2 * x + 1]);
             return e;
         };
-        for (const auto& r : p.recs) {
-            const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;
-            // the launch's span: earliest workgroup start over the XCDs -> latest workgroup end over the XCDs (what a
-            // dispatch trace measures; the XCDs do not start a launch at the same moment)
-            long long span = -1;
+        // the launch's span: earliest workgroup start over the XCDs -> latest workgroup end over the XCDs (what a
+        // dispatch trace measures; the XCDs do not start a launch at the same moment); -1: not executed
+        auto span_of = [](const unsigned long long* t) -> long long {
             unsigned long long s0 = ~0ull, e1 = 0;
             for (int x = 0; x < 8; ++x) {
                 if (!t[2 * x] || !t[2 * x + 1]) continue;
                 s0 = std::min(s0, ~0ull - t[2 * x]);
                 e1 = std::max(e1, t[2 * x + 1]);
             }
-            if (e1 && e1 >= s0) span = (long long)(e1 - s0);
+            return e1 && e1 >= s0 ? (long long)(e1 - s0) : -1;
+        };
+        for (const auto& r : p.recs) {
+            const unsigned long long* t = h.data() + kSlotU64 * (size_t)r.slot;
+            if (r.slot < kSlotsPerRange && p.nsnap > 0 && r.slot < p.used0) {
+                // the encoder graph: every replay's copy (stream-ordered D2H after each replay)
+                for (int q = 0; q < p.nsnap; ++q) {
+                    const long long sp = span_of(p.snap + ((size_t)q * kSlotsPerRange + r.slot) * kSlotU64);
+                    if (sp < 0) continue;
+                    acc[r.cls].launches += 1;
+                    acc[r.cls].total_ms += (double)sp * 1e-5;
+                    acc[r.cls].flops += r.flops;
+                    acc[r.cls].bytes += r.bytes;
+                }
+                continue;
+            }
+            const long long span = span_of(t);
             if (span >= 0 && r.prev >= 0) {    // launch-to-launch period in the stream chain
                 const unsigned long long e0 = last_end(r.prev), e1 = last_end(r.slot);
                 if (e0 && e1 > e0 && e1 - e0 < 100000000ull) {
