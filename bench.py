@@ -859,10 +859,13 @@ def per_image_timing(enc_model, dec_models, arch, H, W, dev, reps=3):
         exact = bool(torch.equal(z, zhat)) and bool(torch.equal(zt[0], zhat[0].permute(1, 2, 0)))
     med = lambda v: round(float(np.median(v)) * 1e3, 2)
     return dict(frame=[H, W], bpp=round(len(bs) * 8.0 / (H * W), 5), enc_ms=med(enc), dec_ms=med(dec),
-                dec_team_ms=med(team), enc_dec_bit_exact=exact,
+                dec_team_ms=med(team), enc_dec_bit_exact=exact, dec_path=dec_models[0].decode_path(),
+                dec_team_mode=dec_models[0].team_stats()["mode"],
                 note="eval_model's per-image Enc/DecTime (batch 1, host clock around synchronize): compress() = "
-                     "lbc_encode + host rANS, decompress() = lbc_decode (raster graph decoder); dec_team_ms: the same "
-                     "stream through one k_dec_team launch (decompress_teams, one batch)")
+                     "lbc_encode + host rANS, decompress() = lbc_decode (one image: the single-image decoder k_dec_one "
+                     "where it applies -- dec_path -- else the raster row graphs); dec_team_ms: the same stream through "
+                     "decompress_teams with one batch of one image (lbc_decode_team hands a single image to lbc_decode: "
+                     "dec_team_mode 'one')")
 
 
 def transform_quality(arch, cfg, dev, H, W, n=4):

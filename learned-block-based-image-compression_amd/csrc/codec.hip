@@ -223,9 +223,19 @@ struct lbc_model {
     std::vector<unsigned long long> team_ts_host;
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
     int team_timeouts = 0;    // team launches that timed out at a barrier and were decoded through lbc_decode instead
-    int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense
+    int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense,
+                              // 3 one image through lbc_decode's single-image decoder (k_dec_one)
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
+    // single-image decoder (k_dec_one, one.hip; lbc_decode of one image): the step's operations, the weight-tile
+    // placement over the grid, the granule buffers and the failure word
+    DevBuf one_ops, one_tiles, one_gran, one_fail, one_rans;
+    std::vector<long long> one_key;
+    OneArgs one_args{};
+    int one_grid = 0;
+    int one_ok = 0;             // the placement fits (0: lbc_decode keeps the graph decoder for single images)
+    int dec_path_last = 0;      // the last lbc_decode: 0 the row graphs, 1 k_dec_one
+    int one_timeouts = 0;       // k_dec_one launches that timed out and were decoded by the row graphs instead
 };
 
 namespace {
@@ -1239,6 +1249,171 @@ int lbc_rans_decode_gpu(lbc_model* m, const uint8_t* const* streams, const size_
     return check_status(m, (size_t)n_streams, s);
 }
 
+// ---------------------------------------------------------------------------------------------- single image
+// k_dec_one's program for this handle (one.hip): the raster step's 12 operations (context net x 4, rANS, decoder x 7,
+// exactly the layers, segments and epilogues run_ctx / run_dec give the graph decoder) and the placement of every weight
+// column tile in the LDS of one workgroup (greedy: each tile to the workgroup holding the fewest tiles of its GEMM, then
+// the least bytes).  Applies to KS[1] = 1 (no layer-0 cache), Mlat <= 256, K <= 1536 per GEMM, weights that fit the
+// grid's LDS; returns with m->one_ok = 0 otherwise.
+static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
+    const std::vector<long long> key = {Hb, Wb, cus, m->net->gen, (long long)m->zpad.p, (long long)m->words.p,
+                                        (long long)m->table_dev.p, (long long)m->st_x.p, (long long)m->cdf16_dev.p,
+                                        (long long)m->tmeta_dev.p, (long long)m->word_base.p, (long long)m->st_status.p,
+                                        (long long)m->st_ptr.p, (long long)m->word_count.p};
+    if (key == m->one_key) return LBC_OK;
+    m->one_ok = 0;
+    m->one_key = key;
+    if (m->l0_on || m->P != 1 || m->M > 256 || cus < 16) return LBC_OK;
+    const Net& n = *m->net;
+    std::vector<OneOp> ops(ONE_MAXOPS);
+    auto gemm_op = [&](int o, const Layer& L, int epi, int sq) {
+        OneOp& q = ops[o];
+        q = OneOp{};
+        q.W = L.W.as<float>();
+        q.bias = L.bias.as<float>();
+        q.K = L.K;
+        q.N = L.N;
+        q.NB16 = L.NB16;
+        q.epi = epi;
+        q.sq = sq;
+        q.gx_src = -1;
+        q.gw = (L.N + 15) / 16 * 16;
+    };
+    auto gran_seg = [&](int o, int src, int k0, int k1) {
+        ops[o].seg[ops[o].nseg++] = OneSeg{ONE_GRAN, src, 0, 0, 0, k0, k1};
+    };
+    auto ztaps = [&](int o) {
+        for (int t = 0; t < 4; ++t)
+            ops[o].seg[ops[o].nseg++] = OneSeg{ONE_ZTAP, -1, 0, TAPS_A[t][0], TAPS_A[t][1], t * m->Cx, (t + 1) * m->Cx};
+    };
+    gemm_op(0, n.ctx0, EPI_LEAKY, 0);  ztaps(0);                       // get_meanscale.0 ('A' 3x3 on the window)
+    gemm_op(1, n.ctx1, EPI_LEAKY, 0);  gran_seg(1, 0, 0, n.ctx1.K);
+    gemm_op(2, n.ctx2, EPI_LEAKY, 0);  gran_seg(2, 1, 0, n.ctx2.K);
+    gemm_op(3, n.ctx3, EPI_CTXIDX, 0); gran_seg(3, 2, 0, n.ctx3.K);
+    ops[4] = OneOp{};                                                 // the rANS decode: y_qnt granules
+    ops[4].N = m->M;
+    ops[4].gw = (m->M + 15) / 16 * 16;
+    ops[4].gx_src = -1;
+    gemm_op(5, n.dec0, EPI_BIAS, 0);   ztaps(5); gran_seg(5, 4, 4 * m->Cx, 4 * m->Cx + m->M);
+    gemm_op(6, n.ig0, EPI_IGDN, 1);    gran_seg(6, 5, 0, n.ig0.K);  ops[6].gx_src = 5;
+    gemm_op(7, n.d1, EPI_BIAS, 0);     gran_seg(7, 6, 0, n.d1.K);
+    gemm_op(8, n.ig1, EPI_IGDN, 1);    gran_seg(8, 7, 0, n.ig1.K);  ops[8].gx_src = 7;
+    gemm_op(9, n.d2, EPI_BIAS, 0);     gran_seg(9, 8, 0, n.d2.K);
+    gemm_op(10, n.ig2, EPI_IGDN, 1);   gran_seg(10, 9, 0, n.ig2.K); ops[10].gx_src = 9;
+    gemm_op(11, n.d3, EPI_CLAMPZ, 0);  gran_seg(11, 10, 0, n.d3.K);
+    if (n.d3.N != m->Cx || n.dec0.K != 4 * m->Cx + m->M || n.ctx0.K != 4 * m->Cx || n.ctx3.N != 2 * m->M) return LBC_OK;
+    // shape checks: K slices of 1..12 k-blocks, granule sources wide enough, segments contiguous
+    for (int o = 0; o < ONE_MAXOPS; ++o) {
+        const OneOp& q = ops[o];
+        if (o == 4) continue;
+        const int nkb = q.K / 16;
+        if (q.K % 16 || nkb < KSPLIT || nkb / KSPLIT > ONE_LL_MAX - 1 || !q.W || !q.bias) return LBC_OK;
+        for (int i = 0; i < q.nseg; ++i) {
+            const OneSeg& sg = q.seg[i];
+            if ((sg.k0 & 15) || (i == 0 ? sg.k0 != 0 : sg.k0 != q.seg[i - 1].k1)) return LBC_OK;
+            if (sg.kind == ONE_GRAN && sg.c0 + sg.k1 - sg.k0 > ops[sg.src].gw) return LBC_OK;
+        }
+        if (q.seg[q.nseg - 1].k1 != q.K) return LBC_OK;
+    }
+    // granule buffers
+    size_t ng = 0;
+    for (const OneOp& q : ops) ng += (size_t)q.gw;
+    int rc;
+    if ((rc = m->one_gran.alloc(ng * 8))) return rc;
+    size_t at = 0;
+    for (OneOp& q : ops) {
+        q.gran = m->one_gran.as<unsigned long long>() + at;
+        at += (size_t)q.gw;
+    }
+    // weight placement: workgroups 0 .. G - 2 hold tiles, G - 1 decodes the stream
+    const int G = cus;
+    const size_t cap_f4 = (160 * 1024 - one_lds_bytes(0)) / 16;
+    std::vector<size_t> load(G, 0);
+    std::vector<int> held(G, 0);
+    std::vector<int4> tiles((size_t)G * ONE_NT_MAX, make_int4(-1, 0, 0, 0));
+    for (int o = 0; o < ONE_MAXOPS; ++o) {
+        if (o == 4) continue;
+        const int nt_n = (ops[o].N + 15) / 16;
+        const size_t sz = (size_t)(ops[o].K / 16) * 64;
+        std::vector<int> of_op(G, 0);
+        for (int nt = 0; nt < nt_n; ++nt) {
+            int best = -1;
+            for (int g = 0; g < G - 1; ++g) {
+                if (held[g] >= ONE_NT_MAX || load[g] + sz > cap_f4) continue;
+                if (best < 0 || of_op[g] < of_op[best] || (of_op[g] == of_op[best] && load[g] < load[best])) best = g;
+            }
+            if (best < 0) return LBC_OK;       // does not fit: the graph decoder keeps single images
+            tiles[(size_t)best * ONE_NT_MAX + held[best]] = make_int4(o, nt, (int)load[best], 0);
+            load[best] += sz;
+            held[best] += 1;
+            of_op[best] += 1;
+        }
+    }
+    size_t wmax = 0;
+    for (size_t l : load) wmax = std::max(wmax, l);
+    if ((rc = dev_upload(m->one_ops, ops.data(), ops.size() * sizeof(OneOp)))) return rc;
+    if ((rc = dev_upload(m->one_tiles, tiles.data(), tiles.size() * sizeof(int4)))) return rc;
+    RansArgs r = rans_args(m);
+    r.rows = 1;
+    r.sparse = 1;
+    if ((rc = dev_upload(m->one_rans, &r, sizeof(r)))) return rc;
+    if ((rc = m->one_fail.alloc(64))) return rc;
+    OneArgs& a = m->one_args;
+    a = OneArgs{};
+    a.ops = m->one_ops.as<OneOp>();
+    a.nops = ONE_MAXOPS;
+    a.rans_op = 4;
+    a.rans_wg = G - 1;
+    a.tiles = m->one_tiles.as<int4>();
+    a.wlds_f4 = (int)wmax;
+    a.zpad = m->zpad.as<float>();
+    a.Hp = Hb + 2;
+    a.Wp = Wb + 4;
+    a.Cx = m->Cx;
+    a.Hb = Hb;
+    a.Wb = Wb;
+    a.rans = m->one_rans.as<RansArgs>();
+    a.Mlat = m->M;
+    a.table = m->table_dev.as<float>();
+    a.fail = m->one_fail.as<unsigned>();
+    a.tmo = 100000000ull;     // 1 s per wait (100 MHz)
+    if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4)) < 1) return LBC_OK;
+    m->one_grid = G;
+    m->one_ok = 1;
+    return LBC_OK;
+}
+
+// One image through k_dec_one when it applies (LBIC_ONE=0 keeps the row graphs: A/B runs).  *used = 1: decoded (zpad
+// holds the reconstruction); 0: not applicable; -1: the launch timed out (counted; the caller decodes with the graphs
+// after re-uploading the stream).
+static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStream_t s, int* used) {
+    *used = 0;
+    const char* e = getenv("LBIC_ONE");
+    if ((e && atoi(e) == 0) || !rans_sparse_choice(lens, 1, (double)Hb * Wb * m->M)) return LBC_OK;
+    int cus = 0, rc;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->cfg.device));
+    if ((rc = one_prepare(m, Hb, Wb, cus))) return rc;
+    if (!m->one_ok) return LBC_OK;
+    OneArgs a = m->one_args;
+    if (const char* t = getenv("LBIC_ONE_TMO")) a.tmo = std::max(1ull, strtoull(t, nullptr, 10));   // test hook
+    HIPCHK(hipMemsetAsync(m->one_gran.p, 0, m->one_gran.bytes, s));
+    HIPCHK(hipMemsetAsync(m->one_fail.p, 0, 64, s));
+    if ((rc = launch_dec_one(a, m->one_grid, s))) return rc;
+    unsigned fail = 0;
+    HIPCHK(hipMemcpyAsync(&fail, m->one_fail.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (fail) {
+        m->one_timeouts += 1;
+        static std::atomic<bool> noted{false};
+        if (!noted.exchange(true))
+            fprintf(stderr, "[lbic] single-image decode: wait timeout, decoding through the row graphs (counted)\n");
+        *used = -1;
+        return LBC_OK;
+    }
+    *used = 1;
+    return LBC_OK;
+}
+
 int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, int n_img, int Hb, int Wb,
                float* zhat_dev, void* stream) {
     if (!m || !streams || !lens || !zhat_dev) return set_error(LBC_E_ARG, "null argument");
@@ -1254,6 +1429,23 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     if ((rc = upload_streams(m, subs, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[2], s));
     HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+    m->dec_path_last = 0;
+    if (n_img == 1) {     // one image: the persistent single-image decoder (one.hip) where it applies
+        int used = 0;
+        if ((rc = decode_one(m, lens, Hb, Wb, s, &used))) return rc;
+        if (used == 1) {
+            m->dec_path_last = 1;
+            if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
+            HIPCHK(hipEventRecord(m->ev[3], s));
+            m->dec_timed = true;
+            return check_status(m, (size_t)n_img, s);
+        }
+        if (used == -1) {   // a timed-out launch advanced the coder state: start again
+            if ((rc = upload_streams(m, subs, s))) return rc;
+            HIPCHK(hipEventRecord(m->ev[2], s));
+            HIPCHK(hipMemsetAsync(m->zpad.p, 0, (size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * sizeof(float), s));
+        }
+    }
     // image groups -> lanes: every lane runs its own raster chain on its own stream, so the small
     // per-step kernels of different groups fill the GPU side by side.  Each lane's block row (Wb raster
     // steps, 13 launches each) is one captured HIP graph replayed Hb times: its kernels read the row
@@ -1521,6 +1713,16 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
             return set_error(LBC_E_ARG, "team decode handles must share one geometry and device");
     }
     const char* te = getenv("LBIC_TEAM");
+    if (T == 1 && n_img == 1 && !(te && atoi(te) == 0)) {
+        // one image: the whole chip is its team -- lbc_decode runs the single-image decoder (k_dec_one) where it
+        // applies, else the row graphs (faster than a team of 32 or 64 workgroups for one image: 0.59 vs 0.75 s per
+        // 768x768 frame, profiles/r04/r04_c5_b1_s*.log)
+        const int rc1 = lbc_decode(ms[0], streams, lens, 1, Hb, Wb, zhat_devs[0], stream);
+        if (rc1) return rc1;
+        ms[0]->team_mode_last = ms[0]->dec_path_last == 1 ? 3 : 0;
+        ms[0]->team_launch_bytes = ms[0]->team_launch_flops = 0;
+        return LBC_OK;
+    }
     const int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
     const double zbytes = (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->Cx * 4;
     const double lbytes = ms[0]->l0_on ? (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->C1P * 4 : 0.0;
@@ -1657,6 +1859,13 @@ int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double*
     *bytes = m->team_launch_bytes;
     *flops = m->team_launch_flops;
     *plain = m->team_plain_last;
+    return LBC_OK;
+}
+
+int lbc_decode_path(const lbc_model* m, int* path, int* timeouts) {
+    if (!m || !path || !timeouts) return set_error(LBC_E_ARG, "null argument");
+    *path = m->dec_path_last;
+    *timeouts = m->one_timeouts;
     return LBC_OK;
 }
 

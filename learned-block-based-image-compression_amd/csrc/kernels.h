@@ -142,6 +142,47 @@ __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
     return S % MT == 0 && L >= 1 && L <= 9 && ni <= TEAM_NI_MAX;
 }
 
+// Single-image decoder (k_dec_one, one.hip): the reference-format raster decode of ONE image in one persistent launch
+// over every CU, each weight column tile of the step's GEMMs resident in the LDS of one workgroup for the whole launch,
+// operations handed over as data-tagged 8-byte granules {value, step + 1} (no barriers)
+constexpr int ONE_MAXOPS = 12;     // operations of a raster step: context net x 4, rANS, decoder x 7
+constexpr int ONE_MAXSEG = 6;
+constexpr int ONE_NT_MAX = 4;      // weight tiles one workgroup holds
+constexpr int ONE_LL_MAX = 12;     // k-blocks of one K slice (K <= 1536)
+enum OneSrc : int { ONE_GRAN = 0, ONE_ZTAP = 1 };
+struct OneSeg {
+    int kind;                // ONE_GRAN: columns [k0, k1) of K are columns [c0, c0 + k1 - k0) of op `src`'s granules;
+    int src, c0;             // ONE_ZTAP: the zpad tap (dy, dx) of the current block, channels [k - k0]
+    int dy, dx;
+    int k0, k1;
+};
+struct OneOp {
+    const float* W;          // packed [K/16][NB16][4][16][4] (GEMMs; null for the rANS operation)
+    const float* bias;
+    int K, N, NB16, epi, sq; // epi: EPI_BIAS / EPI_LEAKY / EPI_IGDN / EPI_GDN / EPI_CTXIDX (value only) / EPI_CLAMPZ
+    int nseg;
+    OneSeg seg[ONE_MAXSEG];
+    int gx_src;              // GDN / IGDN: the op whose granules hold the layer input x
+    unsigned long long* gran;   // this op's output granules [gw] {float bits, step + 1}
+    int gw;                  // granule width (N padded to 16)
+};
+struct OneArgs {
+    const OneOp* ops;        // [nops] device, read-only for the launch
+    int nops, rans_op, rans_wg;
+    const int4* tiles;       // [grid][ONE_NT_MAX] {op, column tile, LDS offset in float4s, 0}; op -1: none
+    int wlds_f4;             // float4s of weight tiles per workgroup (dynamic LDS)
+    float* zpad;
+    int Hp, Wp, Cx, Hb, Wb;
+    const RansArgs* rans;    // device: the stream's coder state / tables (idx, ksi, yq unused: LDS copies)
+    int Mlat;
+    const float* table;      // scale table (64)
+    unsigned* fail;          // failure word (1: a wait timed out), zeroed before the launch
+    unsigned long long tmo;  // s_memrealtime ticks one wait may take
+};
+size_t one_lds_bytes(int wlds_f4);
+int one_blocks_per_cu(size_t lds);
+int launch_dec_one(const OneArgs& a, int grid, hipStream_t s);
+
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
 size_t team_lds_bytes(const TeamArgs& a);   // k_dec_team's dynamic LDS for a launch
 int launch_dec_team(const TeamArgs& a, hipStream_t s);

@@ -612,9 +612,13 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
 // window's first word, [4] valid, [5..6] word base, [7] word count, [64..575] tmeta) between the raster steps, and the
 // window is refilled from global memory only when fewer words than one block can consume remain in it: the step's
 // only global reads are then the block's scale indexes (written by the context net this step).
-template <bool SC1 = false, bool PERSIST = false>
+// LOCAL (k_dec_one): the scale indexes, the context output (scales | means, stride 2 Mlat) and y_qnt are the caller's LDS
+// arrays lidx / lksi / lyq of ONE row instead of a.idx / a.ksi / a.yq
+template <bool SC1 = false, bool PERSIST = false, bool LOCAL = false>
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true,
-                                                const uint16_t* tab = nullptr, uint32_t* lc = nullptr) {
+                                                const uint16_t* tab = nullptr, uint32_t* lc = nullptr,
+                                                const int32_t* lidx = nullptr, const float* lksi = nullptr,
+                                                float* lyq = nullptr) {
     RSTAMP(0);
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
@@ -628,7 +632,8 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     const int Mlat = a.Mlat;
     int ti[4];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) ti[kb] = ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1)) & 63;
+    for (int kb = 0; kb < 4; ++kb)
+        ti[kb] = (LOCAL ? lidx[min(kb * 64 + lane, Mlat - 1)] : ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1))) & 63;
     int t_fb, t_S, t_lm2, t_ca, t_off, t_lf, t_lfm, t_lfp;
     unsigned long long x;
     int p, nw, p0;
@@ -835,7 +840,8 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
         if (i < Mlat) {
-            if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
+            if constexpr (LOCAL) lyq[i] = (float)(symv[kb] + moff[kb]) + lksi[Mlat + i];
+            else if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
             else st<SC1>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + ld<SC1>(a.ksi + (long)row * a.ldk + Mlat + i), wt);
         }
     }

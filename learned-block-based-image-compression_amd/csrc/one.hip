@@ -1,0 +1,360 @@
+// Single-image decoder (gfx950): the reference-format raster decode of ONE image (decompress, net:400-452; the batch-1
+// path of eval_model, agents/blkbsdimgcomp_agent.py:591-599) as one persistent launch over every CU.
+//
+// Why a kernel of its own: at batch 1 a raster step is a chain of 12 dependent operations on ONE row; the graph decoder
+// pays a launch boundary per operation and streams every weight tile from the Infinity Cache every step (25.6 MB per
+// step at B8_lowrate), the team kernel pays a barrier over all its workgroups and the same stream.  Here the weights
+// never move: every column tile of every GEMM of the step (K x 16 fp32, 48-72 KB) is copied ONCE into the LDS of one
+// workgroup (25.6 MB over 256 CUs x ~143 KB of LDS), and an operation is computed by the workgroups holding its tiles
+// as soon as its inputs are there.  Hand-offs are data-tagged granules (MI355X_MICROARCH.md "handoff-1to1"): every
+// output element is stored as one 8-byte {float bits, step + 1} word, write-through (sc1); a consumer polls the
+// granules it needs with sc1 loads until every tag reads the current step, so data and flag arrive together and only the
+// producers and the consumers of an edge take part (no barrier).  The reconstruction goes to zpad as well (write-through,
+// drained before the d3 granules are published), where later steps read their window taps.
+//
+// Arithmetic per output element is k_gemm_s's: the same KSPLIT = 8 K slices, each a k-ordered chain of
+// v_mfma_f32_16x16x4_f32 on the same fragments (row 0 of the 16-row tile carries the image; rows 1-15 are zero), the
+// slice-ordered sum and the same epilogue formulas: bit-identical to lbc_decode's graph decoder
+// (tests/test_one_gpu.py).  The rANS decode is rans_row_sparse on one wave of a workgroup that holds no weights, its
+// coder state persistent in LDS.
+#include "kernels_dev.h"
+
+namespace lbic {
+
+namespace {
+
+constexpr int ONE_RC_WORDS = 576;    // rans_row_sparse's persistent coder-state cache
+constexpr int ONE_SCR = 256;         // floats of A scratch per wave (>= ONE_LL_MAX x 16)
+
+typedef const __attribute__((address_space(4))) OneOp* cop_p;
+
+__device__ __forceinline__ uint4 ld16_sc1(const void* base, unsigned byte_off) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));   // aux 16: sc1
+}
+__device__ __forceinline__ void st_gran(unsigned long long* p, float v, unsigned tag) {
+    const unsigned long long w = ((unsigned long long)tag << 32) | __float_as_uint(v);
+    __hip_atomic_store((gptr<unsigned long long>)p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the epilogue value of k_gemm_s / k_dec_team (kernels_dev.h epilogue) for one output element: the same float operations
+__device__ __forceinline__ float one_epi(int epi, float v, float b, float xv) {
+    switch (epi) {
+        case EPI_LEAKY: {
+            const float t = v + b;
+            return t > 0.f ? t : t * 0.01f;
+        }
+        case EPI_GDN: {
+            const float sq = __fsqrt_rn(v + b);
+            return xv * __fdiv_rn(1.0f, sq);
+        }
+        case EPI_IGDN: {
+            const float sq = __fsqrt_rn(v + b);
+            return xv * sq;
+        }
+        case EPI_CLAMPZ:
+            return fminf(fmaxf(v + b, -0.5f), 0.5f);
+        default:   // EPI_BIAS, EPI_CTXIDX (the value; the rANS workgroup derives the scale index itself)
+            return v + b;
+    }
+}
+
+struct OneCtl {
+    unsigned* fail;
+    unsigned long long tmo;
+};
+
+// Wait until granules [g0, g0 + cnt) of `gran` carry `tag`, then leave their values in scr[0, cnt) (LDS).  One wave;
+// pairs of granules per lane (g0 even).  Returns false when the launch failed (timeout here or elsewhere).
+__device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, int g0, int cnt, unsigned tag, float* scr,
+                                               const OneCtl& c) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        bool ok = true;
+        uint4 q[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int j = (p * 64 + lane) * 2;
+            q[p] = ld16_sc1(gran, (unsigned)(g0 + min(j, max(cnt - 2, 0))) * 8u);
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int j = (p * 64 + lane) * 2;
+            if (j < cnt) ok &= q[p].y == tag && (j + 1 >= cnt || q[p].w == tag);
+        }
+        if (__ballot(!ok) == 0ull) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int j = (p * 64 + lane) * 2;
+                if (j < cnt) scr[j] = __uint_as_float(q[p].x);
+                if (j + 1 < cnt) scr[j + 1] = __uint_as_float(q[p].z);
+            }
+            return true;
+        }
+        if (__hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
+            if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// my[i] without dynamic indexing into a register array (which would put the array in scratch)
+__device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
+    int4 r = my[0];
+#pragma unroll
+    for (int j = 1; j < ONE_NT_MAX; ++j) r = i == j ? my[j] : r;
+    return r;
+}
+
+// the segment of k-block kb (uniform)
+__device__ __forceinline__ int seg_of(const OneOp& op, int kb) {
+    const int k = kb << 4;
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < ONE_MAXSEG; ++i) s = (i < op.nseg && k >= op.seg[i].k0) ? i : s;
+    return s;
+}
+
+// One GEMM operation: the tiles of `op` this workgroup holds (my[]), for block (v, h) at step tag - 1.  Every thread
+// returns the same value (false: the launch failed).
+template <int LL>
+__device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v,
+                                         int h, unsigned tag, const f4* wl, float* red, float* scr_all, int* sflag,
+                                         const OneCtl& c) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nkb = op.K >> 4;
+    const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
+    float* scr = scr_all + wave * ONE_SCR;
+    bool ok = true;
+    // window taps: every zpad write of the steps before this one is visible once the last operation of the previous
+    // step (d3, whose producers drain their zpad stores before publishing) reads step `tag - 1`
+    bool ztap = false;
+    for (int s = 0; s < op.nseg; ++s) {
+        const int kk0 = op.seg[s].k0 >> 4, kk1 = op.seg[s].k1 >> 4;
+        ztap |= op.seg[s].kind == ONE_ZTAP && kk0 < kb0 + n && kk1 > kb0;
+    }
+    if (ztap && tag > 1) {
+        const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));
+        for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
+            ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), tag - 1, scr, c);
+    }
+    // granule k-blocks of this slice: wait for them (the current step's tag), values into the wave's scratch
+    for (int cb = 0; cb < n && ok;) {
+        const int s = seg_of(op, kb0 + cb);
+        const OneSeg& sg = op.seg[s];
+        int ce = cb + 1;
+        while (ce < n && seg_of(op, kb0 + ce) == s) ++ce;
+        if (sg.kind == ONE_GRAN) {
+            const OneOp& src = *(const OneOp*)((cop_p)a.ops + sg.src);
+            const int g0 = sg.c0 + ((kb0 + cb) << 4) - sg.k0;
+            ok = wave_wait_gran(src.gran, g0, (ce - cb) * 16, tag, scr + cb * 16, c);
+        }
+        cb = ce;
+    }
+    // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
+    __builtin_amdgcn_wave_barrier();
+    f4 av[LL];
+    const bool row0 = (lane & 15) == 0;
+    const int q4 = (lane >> 4) * 4;
+    const long cell = ((long)(v + 2) * a.Wp + (h + 2));
+#pragma unroll
+    for (int cc = 0; cc < LL; ++cc) {
+        const int ci = min(cc, n - 1);
+        const int kb = kb0 + ci;
+        const int s = seg_of(op, kb);
+        const OneSeg& sg = op.seg[s];
+        f4 x = f4{0.f, 0.f, 0.f, 0.f};
+        if (sg.kind == ONE_ZTAP) {
+            const unsigned off = (unsigned)((cell + (long)sg.dy * a.Wp + sg.dx) * a.Cx + (kb << 4) - sg.k0 + q4) * 4u;
+            const uint4 u = ld16_sc1(a.zpad, off);
+            x = row0 ? __builtin_bit_cast(f4, u) : x;
+        } else {
+            const f4 u = *reinterpret_cast<const f4*>(scr + ci * 16 + q4);
+            x = row0 ? u : x;
+        }
+        if (op.sq) x = x * x;
+        av[cc] = x;
+    }
+    // every tile of this op the workgroup holds: chain, partials, slice-ordered sum, epilogue, publish
+    const int N = op.N, gw = op.gw;
+    for (int i = 0; i < ONE_NT_MAX; ++i) {
+        const int4 ti = pick(my, i);
+        if (ti.x != o) continue;
+        const int nt = ti.y;
+        const f4* wt = wl + ti.z + lane;
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        f4 wv[LL];
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + min(cc, n - 1)) * 64];
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) {
+            f4 t = acc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cc][e], wv[cc][e], t, 0, 0, 0);
+            acc = cc < n ? t : acc;
+        }
+        if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            const int e = threadIdx.x, col = nt * 16 + e;
+            float vv = red[e];
+#pragma unroll
+            for (int s = 1; s < KSPLIT; ++s) vv += red[s * 16 + e];
+            float out = 0.f;
+            if (col < N) {
+                float xv = 0.f;
+                if (op.epi == EPI_GDN || op.epi == EPI_IGDN) {
+                    const OneOp& gx = *(const OneOp*)((cop_p)a.ops + op.gx_src);
+                    xv = __uint_as_float(ld16_sc1(gx.gran, (unsigned)(col & ~1) * 8u).x);
+                    if (col & 1) xv = __uint_as_float(ld16_sc1(gx.gran, (unsigned)(col & ~1) * 8u).z);
+                }
+                out = one_epi(op.epi, vv, op.bias[col], xv);
+                if (op.epi == EPI_CLAMPZ) {
+                    st<true>(a.zpad + cell * a.Cx + col, out, true);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tap data before the granule
+                }
+            }
+            if (col < gw) st_gran(op.gran + col, out, tag);
+        }
+        __syncthreads();
+    }
+    // a uniform verdict for the whole workgroup
+    if (!ok && lane == 0) *sflag = 1;
+    __syncthreads();
+    const bool good = *sflag == 0;
+    __syncthreads();
+    return good;
+}
+
+__device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v, int h,
+                             unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c) {
+    switch ((op.K >> 4) / KSPLIT) {
+#define LBIC_ONE(L_) \
+    case L_: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
+        LBIC_ONE(0) LBIC_ONE(1) LBIC_ONE(2) LBIC_ONE(3) LBIC_ONE(4) LBIC_ONE(5) LBIC_ONE(6) LBIC_ONE(7) LBIC_ONE(8)
+        LBIC_ONE(9) LBIC_ONE(10) LBIC_ONE(11)
+#undef LBIC_ONE
+        default: return false;   // (the host admits K <= 1536 only)
+    }
+}
+
+}  // namespace
+
+// dynamic LDS: [weight tiles wlds_f4 float4s][partials KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
+// [rANS state cache ONE_RC_WORDS][idx 256][ksi 512][yq 256][flag 4 words]
+size_t one_lds_bytes(int wlds_f4) {
+    return (size_t)wlds_f4 * 16 + (size_t)(KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
+           (size_t)(RANS_WIN + ONE_RC_WORDS + 256 + 512 + 256 + 4) * 4;
+}
+
+__global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t one_lds[];
+    f4* wl = reinterpret_cast<f4*>(one_lds);
+    float* red = reinterpret_cast<float*>(wl + a.wlds_f4);
+    float* scr = red + KSPLIT * 16;
+    uint32_t* lwin = reinterpret_cast<uint32_t*>(scr + KSPLIT * ONE_SCR);
+    uint32_t* rcache = lwin + RANS_WIN;
+    int32_t* l_idx = reinterpret_cast<int32_t*>(rcache + ONE_RC_WORDS);
+    float* l_ksi = reinterpret_cast<float*>(l_idx + 256);
+    float* l_yq = l_ksi + 512;
+    int* sflag = reinterpret_cast<int*>(l_yq + 256);
+    const int rank = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const OneCtl c{a.fail, a.tmo};
+    int4 my[ONE_NT_MAX];
+#pragma unroll
+    for (int i = 0; i < ONE_NT_MAX; ++i) my[i] = a.tiles[rank * ONE_NT_MAX + i];
+    // this workgroup's weight tiles into LDS, once (read-only for the launch)
+#pragma unroll
+    for (int i = 0; i < ONE_NT_MAX; ++i) {
+        if (my[i].x < 0) continue;
+        const OneOp& op = *(const OneOp*)((cop_p)a.ops + my[i].x);
+        const f4* src = reinterpret_cast<const f4*>(op.W);
+        const int nkb = op.K >> 4;
+        for (int j = threadIdx.x; j < nkb * 64; j += blockDim.x) {
+            const int kb = j >> 6, l = j & 63;
+            wl[my[i].z + j] = src[((long)kb * op.NB16 + my[i].y) * 64 + l];
+        }
+    }
+    if (threadIdx.x == 0) {
+        rcache[4] = 0u;    // no cached coder state yet
+        *sflag = 0;
+    }
+    __syncthreads();
+    const RansArgs& R = *(const RansArgs*)((const __attribute__((address_space(4))) RansArgs*)a.rans);
+    for (int t = 0; t < a.Hb * a.Wb; ++t) {
+        const int v = t / a.Wb, h = t - v * a.Wb;
+        const unsigned tag = (unsigned)t + 1u;
+        for (int o = 0; o < a.nops; ++o) {
+            if (o == a.rans_op) {
+                if (rank != a.rans_wg) continue;
+                bool ok = true;
+                if (wave == 0) {
+                    // scales | means of the context net (2 Mlat granules), scale indexes (build_indexes) into LDS
+                    const OneOp& ctx = *(const OneOp*)((cop_p)a.ops + (o - 1));
+                    const int M = a.Mlat;
+                    for (int g0 = 0; g0 < 2 * M && ok; g0 += 256)
+                        ok = wave_wait_gran(ctx.gran, g0, min(256, 2 * M - g0), tag, l_ksi + g0, c);
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    __builtin_amdgcn_wave_barrier();
+                    for (int i = lane; i < M; i += 64) l_idx[i] = scale_index(l_ksi[i], a.table);
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    __builtin_amdgcn_wave_barrier();
+                    if (ok) {
+                        rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, nullptr, rcache, l_idx, l_ksi, l_yq);
+                        __builtin_amdgcn_s_waitcnt(0xC07F);
+                        __builtin_amdgcn_wave_barrier();
+                        const OneOp& yo = *(const OneOp*)((cop_p)a.ops + o);
+                        for (int i = lane; i < yo.gw; i += 64) st_gran(yo.gran + i, i < M ? l_yq[i] : 0.f, tag);
+                    }
+                    if (!ok && lane == 0) *sflag = 1;
+                }
+                __syncthreads();
+                const bool good = *sflag == 0;
+                __syncthreads();
+                if (!good) return;
+                continue;
+            }
+            bool mine = false;
+#pragma unroll
+            for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
+            if (!mine) continue;
+            const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
+            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c)) return;
+        }
+    }
+}
+
+int one_blocks_per_cu(size_t lds) {
+    int nb = 0;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_one), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_one), 512, lds) !=
+        hipSuccess)
+        return 0;
+    return nb;
+}
+
+int launch_dec_one(const OneArgs& a, int grid, hipStream_t s) {
+    if (!a.ops || !a.tiles || !a.rans || !a.fail || !a.zpad || a.nops < 2 || a.nops > ONE_MAXOPS || grid < 2 ||
+        a.rans_wg < 0 || a.rans_wg >= grid || a.rans_op < 1 || a.rans_op >= a.nops || a.Mlat > 256 || a.Mlat < 1)
+        return set_error(LBC_E_ARG, "bad single-image decoder arguments");
+    const size_t lds = one_lds_bytes(a.wlds_f4);
+    if (lds > 160 * 1024) return set_error(LBC_E_ARG, "single-image decoder: LDS image too large");
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_one), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(k_dec_one, dim3(grid), dim3(512), lds, s, a);
+    return launch_status("k_dec_one");
+}
+
+}  // namespace lbic

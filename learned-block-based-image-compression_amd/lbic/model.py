@@ -256,8 +256,15 @@ class BlockBasedImgCompLossyNetv9:
         rq = ctypes.c_int()
         _lib.check(L.lbc_team_ring(self._h, ctypes.byref(rq)))
         return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value,
-                    mode=("fallback", "team_sparse", "team_dense")[mode.value], sc1_reruns=rr.value,
+                    mode=("fallback", "team_sparse", "team_dense", "one")[mode.value], sc1_reruns=rr.value,
                     timeout_fallbacks=to.value, ring_slots=rq.value)
+
+    def decode_path(self):
+        """How the last decompress of this handle ran (lbc_decode_path): dict(path="graphs" | "one", one_timeouts) --
+        "one" = the single-image persistent decoder k_dec_one (one image, low rate, KS[1] = 1)."""
+        p, t = ctypes.c_int(), ctypes.c_int()
+        _lib.check(_lib.lib().lbc_decode_path(self._h, ctypes.byref(p), ctypes.byref(t)))
+        return dict(path=("graphs", "one")[p.value], one_timeouts=t.value)
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]

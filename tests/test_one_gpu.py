@@ -1,0 +1,114 @@
+"""The single-image decoder (k_dec_one, csrc/one.hip): lbc_decode of ONE image -- the reference's own per-image path,
+decompress() (graphs/models/BlockBasedImgCompLossy_net.py:400-452) as eval_model calls it
+(agents/blkbsdimgcomp_agent.py:591-599) -- as one persistent launch with every weight tile resident in LDS.
+
+* The reference's stream of every KS3111 closed-loop fixture (re-made by the oracle coder from the fixture's symbols and
+  indexes) decoded by k_dec_one equals the fixture's ``zhat_dec`` (the reference's decompress()) within 1e-5 relative,
+  and equals the row-graph decoder (LBIC_ONE=0) bit for bit.
+* Library-encoded frames of ragged shapes (one block row, one block column, two columns, odd sizes) decode bit-exactly
+  to the encoder's reconstruction, through k_dec_one.
+* The full 768x768 B8_lowrate frame: tests/test_fullsize_gpu.py::test_full_frame_b8_lowrate_vs_reference decodes it as
+  one image, i.e. through k_dec_one (asserted there).
+* A launch whose waits time out (LBIC_ONE_TMO=1 tick) is decoded by the row graphs instead, counted, same result.
+* Geometries it does not cover (KS[1] = 3: the layer-0 cache; several images) keep the row graphs.
+"""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_rel, golden_arch, golden_rate, load_golden
+from lbic.weights import synth_state_dict
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+_M = {}
+
+
+def _model(arch, seed, rate):
+    from lbic.model import BlockBasedImgCompLossyNetv9
+    key = (arch, seed, rate)
+    if key not in _M:
+        cfg = types.SimpleNamespace(block_size=arch.B, KS=list(arch.KS), N=arch.N, M=arch.M, gpu_device=0)
+        m = BlockBasedImgCompLossyNetv9(cfg)
+        m.load_state_dict(synth_state_dict(arch, seed, rate=rate))
+        m.update(force=True)
+        _M[key] = m
+    return _M[key]
+
+
+@pytest.mark.parametrize("name", ["tiny_ks3111", "b8_lowrate_2rows", "b16_lowrate", "b16_lowrate_low"])
+def test_one_decodes_reference_stream(name, monkeypatch):
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")       # k_dec_one decodes with the sparse rANS variant (any rate)
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    Hb, Wb = g["x"].shape[:2]
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
+    z1 = m.decompress_batch([stream], Hb, Wb)
+    path = m.decode_path()
+    monkeypatch.setenv("LBIC_ONE", "0")
+    zg = m.decompress_batch([stream], Hb, Wb)
+    assert m.decode_path()["path"] == "graphs"
+    ref = g["zhat_dec"]
+    assert_rel(z1[0].cpu().numpy(), ref, what=f"{name}: single-image decode vs the reference's decompress()")
+    assert torch.equal(z1, zg), f"{name}: k_dec_one != row graphs ({(z1 != zg).sum().item()} values)"
+    print(f"{name} (N{arch.N} B{arch.B}, {Hb}x{Wb} blocks): path {path['path']}, "
+          f"max |zhat - zhat_dec(ref)| = {float(np.abs(z1[0].cpu().numpy() - ref).max()):.3e}")
+    if name in ("tiny_ks3111", "b8_lowrate_2rows"):
+        assert path["path"] == "one", path
+
+
+@pytest.mark.parametrize("Hb,Wb", [(1, 7), (5, 1), (3, 2), (4, 9), (2, 96)])
+def test_one_roundtrip_ragged(Hb, Wb):
+    from lbic.arch import Arch
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    m = _model(arch, 1337, "low")
+    x = torch.from_numpy(np.random.default_rng(Hb * 100 + Wb).integers(0, 256, (1, Hb, Wb, arch.cx))
+                         .astype(np.float32) / 255.0 - 0.5).cuda()
+    r = m.compress_batch(x)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    z = m.decompress_batch(st, Hb, Wb)
+    assert m.decode_path()["path"] == "one"
+    assert torch.equal(z, r["zhat"]), f"{Hb}x{Wb}: decode != encode"
+
+
+def test_one_timeout_falls_back(monkeypatch):
+    from lbic.arch import Arch
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    m = _model(arch, 1337, "low")
+    x = torch.from_numpy(np.random.default_rng(5).integers(0, 256, (1, 3, 4, arch.cx))
+                         .astype(np.float32) / 255.0 - 0.5).cuda()
+    r = m.compress_batch(x)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    t0 = m.decode_path()["one_timeouts"]
+    monkeypatch.setenv("LBIC_ONE_TMO", "1")
+    z = m.decompress_batch(st, 3, 4)
+    p = m.decode_path()
+    assert p["path"] == "graphs" and p["one_timeouts"] == t0 + 1, p
+    assert torch.equal(z, r["zhat"])
+    monkeypatch.delenv("LBIC_ONE_TMO")
+    z = m.decompress_batch(st, 3, 4)
+    assert m.decode_path()["path"] == "one"
+    assert torch.equal(z, r["zhat"])
+
+
+def test_one_not_for_layer0_cache_or_batches():
+    g = load_golden("loop_tiny_ks3311")
+    arch = golden_arch(g)
+    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    Hb, Wb = g["x"].shape[:2]
+    z = m.decompress_batch([stream], Hb, Wb)
+    assert m.decode_path()["path"] == "graphs"            # KS[1] = 3: the layer-0 cache is not in k_dec_one
+    assert_rel(z[0].cpu().numpy(), g["zhat_dec"])
+    g = load_golden("loop_tiny_ks3111")
+    arch = golden_arch(g)
+    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    Hb, Wb = g["x"].shape[:2]
+    z = m.decompress_batch([stream, stream], Hb, Wb)
+    assert m.decode_path()["path"] == "graphs"            # two images: the row graphs
+    assert torch.equal(z[0], z[1])
