@@ -1302,12 +1302,12 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     gemm_op(10, n.ig2, EPI_IGDN, 1);   gran_seg(10, 9, 0, n.ig2.K); ops[10].gx_src = 9;
     gemm_op(11, n.d3, EPI_CLAMPZ, 0);  gran_seg(11, 10, 0, n.d3.K);
     if (n.d3.N != m->Cx || n.dec0.K != 4 * m->Cx + m->M || n.ctx0.K != 4 * m->Cx || n.ctx3.N != 2 * m->M) return LBC_OK;
-    // shape checks: K slices of 1..12 k-blocks, granule sources wide enough, segments contiguous
+    // shape checks: K slices of 0..12 k-blocks, granule sources wide enough, segments contiguous
     for (int o = 0; o < ONE_MAXOPS; ++o) {
         const OneOp& q = ops[o];
         if (o == 4) continue;
         const int nkb = q.K / 16;
-        if (q.K % 16 || nkb < KSPLIT || nkb / KSPLIT > ONE_LL_MAX - 1 || !q.W || !q.bias) return LBC_OK;
+        if (q.K % 16 || nkb < 1 || nkb / KSPLIT > ONE_LL_MAX - 1 || !q.W || !q.bias) return LBC_OK;
         for (int i = 0; i < q.nseg; ++i) {
             const OneSeg& sg = q.seg[i];
             if ((sg.k0 & 15) || (i == 0 ? sg.k0 != 0 : sg.k0 != q.seg[i - 1].k1)) return LBC_OK;

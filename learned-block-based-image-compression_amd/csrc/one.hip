@@ -164,7 +164,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     const long cell = ((long)(v + 2) * a.Wp + (h + 2));
 #pragma unroll
     for (int cc = 0; cc < LL; ++cc) {
-        const int ci = min(cc, n - 1);
+        const int ci = max(min(cc, n - 1), 0);      // (an empty slice, n = 0, loads k-block kb0 and adds nothing)
         const int kb = kb0 + ci;
         const int s = seg_of(op, kb);
         const OneSeg& sg = op.seg[s];
@@ -190,7 +190,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         f4 acc = f4{0.f, 0.f, 0.f, 0.f};
         f4 wv[LL];
 #pragma unroll
-        for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + min(cc, n - 1)) * 64];
+        for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
             f4 t = acc;
