@@ -54,7 +54,9 @@ MID_DEFAULT = (1.0, 0.3)
 # rate="low" latent gain per architecture (default LOW_Y_GAIN): B16_lowrate's published point is 0.120 bpp, which the
 # default gain undershoots (0.07 bpp on noise frames); calibrated by tests/golden/tune_mid_rate.py (LOW_TARGETS)
 LOW_POINTS = {   # (B, N, M) -> latent gain; calibration bpp on a noise frame
-    (16, 1280, 192): 0.4905,    # B16_lowrate: 0.1211 bpp on a 128x128 noise frame (published 0.120)
+    (16, 1280, 192): 0.4762,    # B16_lowrate: 0.1204 bpp on the bench's 2048x2048 noise frames (published 0.120;
+                                # tools/calib_low_gpu.py, profiles/r04/r04_c7_calib.log; 0.4905 gave 0.121 on a 128x128
+                                # frame but 0.135 at 2048x2048)
 }
 
 
