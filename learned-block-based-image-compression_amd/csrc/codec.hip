@@ -229,7 +229,8 @@ struct lbc_model {
     double team_launch_bytes = 0, team_launch_flops = 0;
     // single-image decoder (k_dec_one, one.hip; lbc_decode of one image): the step's operations, the weight-tile
     // placement over the grid, the granule buffers and the failure word
-    DevBuf one_ops, one_tiles, one_gran, one_fail, one_rans;
+    DevBuf one_ops, one_tiles, one_gran, one_fail, one_rans, one_ts;
+    std::vector<unsigned long long> one_ts_host;
     std::vector<long long> one_key;
     OneArgs one_args{};
     int one_grid = 0;
@@ -1377,6 +1378,9 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.table = m->table_dev.as<float>();
     a.fail = m->one_fail.as<unsigned>();
     a.tmo = 100000000ull;     // 1 s per wait (100 MHz)
+    a.lazy_z = Wb >= 3 ? 1 : 0;
+    a.ts_step = (Hb / 2) * Wb + Wb / 2;
+    if ((rc = m->one_ts.alloc(ONE_MAXOPS * 4 * sizeof(unsigned long long)))) return rc;
     if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4)) < 1) return LBC_OK;
     m->one_grid = G;
     m->one_ok = 1;
@@ -1396,9 +1400,20 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     if (!m->one_ok) return LBC_OK;
     OneArgs a = m->one_args;
     if (const char* t = getenv("LBIC_ONE_TMO")) a.tmo = std::max(1ull, strtoull(t, nullptr, 10));   // test hook
+    const char* st = getenv("LBIC_ONE_STAMPS");
+    std::vector<unsigned long long> ts0(ONE_MAXOPS * 4, 0ull);
+    if (st && atoi(st)) {
+        for (int o = 0; o < ONE_MAXOPS; ++o) ts0[o * 4] = ~0ull;
+        HIPCHK(hipMemcpyAsync(m->one_ts.p, ts0.data(), ts0.size() * 8, hipMemcpyHostToDevice, s));
+        a.ts = m->one_ts.as<unsigned long long>();
+    }
     HIPCHK(hipMemsetAsync(m->one_gran.p, 0, m->one_gran.bytes, s));
     HIPCHK(hipMemsetAsync(m->one_fail.p, 0, 64, s));
     if ((rc = launch_dec_one(a, m->one_grid, s))) return rc;
+    if (a.ts) {
+        m->one_ts_host.assign(ONE_MAXOPS * 4, 0ull);
+        HIPCHK(hipMemcpyAsync(m->one_ts_host.data(), a.ts, ONE_MAXOPS * 4 * 8, hipMemcpyDeviceToHost, s));
+    }
     unsigned fail = 0;
     HIPCHK(hipMemcpyAsync(&fail, m->one_fail.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1859,6 +1874,14 @@ int lbc_team_stats(const lbc_model* m, double* launch_ms, double* bytes, double*
     *bytes = m->team_launch_bytes;
     *flops = m->team_launch_flops;
     *plain = m->team_plain_last;
+    return LBC_OK;
+}
+
+int lbc_one_stamps(const lbc_model* m, unsigned long long* out, int max_out, int* n_out) {
+    if (!m || !out || !n_out) return set_error(LBC_E_ARG, "null argument");
+    const int n = std::min(max_out, (int)m->one_ts_host.size());
+    for (int i = 0; i < n; ++i) out[i] = m->one_ts_host[i];
+    *n_out = n;
     return LBC_OK;
 }
 

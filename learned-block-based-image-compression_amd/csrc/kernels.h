@@ -178,6 +178,10 @@ struct OneArgs {
     const float* table;      // scale table (64)
     unsigned* fail;          // failure word (1: a wait timed out), zeroed before the launch
     unsigned long long tmo;  // s_memrealtime ticks one wait may take
+    int lazy_z;              // 1 (Wb >= 3): a d3 producer drains its zpad store of step t only before publishing step t + 1
+    int ts_step;             // the sampled raster step of `ts`
+    unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step: [0] first workgroup in, [1] last
+                             // workgroup's partials reduced (inputs waited + chains), [2] last one published
 };
 size_t one_lds_bytes(int wlds_f4);
 int one_blocks_per_cu(size_t lds);

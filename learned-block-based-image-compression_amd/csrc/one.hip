@@ -66,8 +66,9 @@ struct OneCtl {
 
 // Wait until granules [g0, g0 + cnt) of `gran` carry `tag`, then leave their values in scr[0, cnt) (LDS).  One wave;
 // pairs of granules per lane (g0 even).  Returns false when the launch failed (timeout here or elsewhere).
+// ge: every tag >= `tag` (a visibility proxy: granules are only ever overwritten by later steps), no values kept
 __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, int g0, int cnt, unsigned tag, float* scr,
-                                               const OneCtl& c) {
+                                               const OneCtl& c, bool ge = false) {
     const int lane = threadIdx.x & 63;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -81,9 +82,11 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int j = (p * 64 + lane) * 2;
-            if (j < cnt) ok &= q[p].y == tag && (j + 1 >= cnt || q[p].w == tag);
+            if (j < cnt)
+                ok &= ge ? (q[p].y >= tag && (j + 1 >= cnt || q[p].w >= tag)) : (q[p].y == tag && (j + 1 >= cnt || q[p].w == tag));
         }
         if (__ballot(!ok) == 0ull) {
+            if (ge) return true;
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 const int j = (p * 64 + lane) * 2;
@@ -109,6 +112,13 @@ __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     return r;
 }
 
+__device__ __forceinline__ float pick_f(const float (&v)[ONE_NT_MAX], int i) {
+    float r = v[0];
+#pragma unroll
+    for (int j = 1; j < ONE_NT_MAX; ++j) r = i == j ? v[j] : r;
+    return r;
+}
+
 // the segment of k-block kb (uniform)
 __device__ __forceinline__ int seg_of(const OneOp& op, int kb) {
     const int k = kb << 4;
@@ -130,19 +140,22 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
     float* scr = scr_all + wave * ONE_SCR;
     bool ok = true;
-    // window taps: every zpad write of the steps before this one is visible once the last operation of the previous
-    // step (d3, whose producers drain their zpad stores before publishing) reads step `tag - 1`
-    bool ztap = false;
-    for (int s = 0; s < op.nseg; ++s) {
-        const int kk0 = op.seg[s].k0 >> 4, kk1 = op.seg[s].k1 >> 4;
-        ztap |= op.seg[s].kind == ONE_ZTAP && kk0 < kb0 + n && kk1 > kb0;
+    const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
+    const int t = (int)tag - 1;
+    // the epilogue operands of this op's tiles (bias: read-only), requested before anything waits
+    float bb[ONE_NT_MAX];
+#pragma unroll
+    for (int i = 0; i < ONE_NT_MAX; ++i) {
+        const int4 ti = my[i];
+        bb[i] = ti.x == o ? op.bias[min(ti.y * 16 + (lane & 15), op.N - 1)] : 0.f;
     }
-    if (ztap && tag > 1) {
-        const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));
-        for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
-            ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), tag - 1, scr, c);
-    }
-    // granule k-blocks of this slice: wait for them (the current step's tag), values into the wave's scratch
+    // inputs of this wave's K slice, run by run of k-blocks of one segment:
+    //  * granules of an earlier op of this step (tag): values into the wave's scratch;
+    //  * the left window tap (0, -1) for h >= 1: the previous step's d3 granules (tag - 1) ARE that block -- values into
+    //    the scratch, no zpad round trip;
+    //  * the taps of the row above: zpad, visible once d3's granules have reached the producing step t' (+ 1, or + 2
+    //    with lazy drains: a d3 producer drains its zpad store of step t' only before publishing step t' + 1)
+    unsigned zneed = 0;
     for (int cb = 0; cb < n && ok;) {
         const int s = seg_of(op, kb0 + cb);
         const OneSeg& sg = op.seg[s];
@@ -152,8 +165,18 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             const OneOp& src = *(const OneOp*)((cop_p)a.ops + sg.src);
             const int g0 = sg.c0 + ((kb0 + cb) << 4) - sg.k0;
             ok = wave_wait_gran(src.gran, g0, (ce - cb) * 16, tag, scr + cb * 16, c);
+        } else if (sg.dy == 0 && sg.dx == -1) {
+            if (h >= 1) ok = wave_wait_gran(last.gran, ((kb0 + cb) << 4) - sg.k0, (ce - cb) * 16, tag - 1, scr + cb * 16, c);
+        } else {
+            const int vv = v + sg.dy, hh = h + sg.dx;
+            if (vv >= 0 && vv < a.Hb && hh >= 0 && hh < a.Wb)
+                zneed = max(zneed, (unsigned)(vv * a.Wb + hh) + (a.lazy_z ? 2u : 1u));
         }
         cb = ce;
+    }
+    if (zneed && ok) {
+        for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
+            ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), zneed, scr + 240, c, true);
     }
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
@@ -169,7 +192,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         const int s = seg_of(op, kb);
         const OneSeg& sg = op.seg[s];
         f4 x = f4{0.f, 0.f, 0.f, 0.f};
-        if (sg.kind == ONE_ZTAP) {
+        if (sg.kind == ONE_ZTAP && !(sg.dy == 0 && sg.dx == -1 && h >= 1)) {
             const unsigned off = (unsigned)((cell + (long)sg.dy * a.Wp + sg.dx) * a.Cx + (kb << 4) - sg.k0 + q4) * 4u;
             const uint4 u = ld16_sc1(a.zpad, off);
             x = row0 ? __builtin_bit_cast(f4, u) : x;
@@ -200,6 +223,8 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         }
         if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
         __syncthreads();
+        if (a.ts && t == a.ts_step && threadIdx.x == 0)
+            atomicMax(a.ts + o * 4 + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (threadIdx.x < 16) {
             const int e = threadIdx.x, col = nt * 16 + e;
             float vv = red[e];
@@ -209,20 +234,28 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             if (col < N) {
                 float xv = 0.f;
                 if (op.epi == EPI_GDN || op.epi == EPI_IGDN) {
-                    const OneOp& gx = *(const OneOp*)((cop_p)a.ops + op.gx_src);
-                    xv = __uint_as_float(ld16_sc1(gx.gran, (unsigned)(col & ~1) * 8u).x);
-                    if (col & 1) xv = __uint_as_float(ld16_sc1(gx.gran, (unsigned)(col & ~1) * 8u).z);
+                    // the layer input x = this op's A operand (one granule segment from k = 0): the values the wave that
+                    // owns column col's k-block left in its scratch
+                    const int kbc = col >> 4;
+                    int w = 0;
+#pragma unroll
+                    for (int q = 1; q < KSPLIT; ++q) w = q * nkb / KSPLIT <= kbc ? q : w;
+                    xv = scr_all[w * ONE_SCR + col - (w * nkb / KSPLIT) * 16];
                 }
-                out = one_epi(op.epi, vv, op.bias[col], xv);
+                out = one_epi(op.epi, vv, pick_f(bb, i), xv);
                 if (op.epi == EPI_CLAMPZ) {
+                    // lazy: this thread's previous zpad store (step t - 1) drained now, the current one by step t + 1
+                    if (a.lazy_z) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     st<true>(a.zpad + cell * a.Cx + col, out, true);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tap data before the granule
+                    if (!a.lazy_z) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tap data before the granule
                 }
             }
             if (col < gw) st_gran(op.gran + col, out, tag);
         }
         __syncthreads();
     }
+    if (a.ts && t == a.ts_step && threadIdx.x == 0)
+        atomicMax(a.ts + o * 4 + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     // a uniform verdict for the whole workgroup
     if (!ok && lane == 0) *sflag = 1;
     __syncthreads();
@@ -295,6 +328,8 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
             if (o == a.rans_op) {
                 if (rank != a.rans_wg) continue;
                 bool ok = true;
+                const bool stamp = a.ts && t == a.ts_step && threadIdx.x == 0;
+                if (stamp) a.ts[o * 4] = __builtin_amdgcn_s_memrealtime();
                 if (wave == 0) {
                     // scales | means of the context net (2 Mlat granules), scale indexes (build_indexes) into LDS
                     const OneOp& ctx = *(const OneOp*)((cop_p)a.ops + (o - 1));
@@ -303,6 +338,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                         ok = wave_wait_gran(ctx.gran, g0, min(256, 2 * M - g0), tag, l_ksi + g0, c);
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
+                    if (stamp) a.ts[o * 4 + 1] = __builtin_amdgcn_s_memrealtime();
                     for (int i = lane; i < M; i += 64) l_idx[i] = scale_index(l_ksi[i], a.table);
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
@@ -312,6 +348,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                         __builtin_amdgcn_wave_barrier();
                         const OneOp& yo = *(const OneOp*)((cop_p)a.ops + o);
                         for (int i = lane; i < yo.gw; i += 64) st_gran(yo.gran + i, i < M ? l_yq[i] : 0.f, tag);
+                        if (stamp) a.ts[o * 4 + 2] = __builtin_amdgcn_s_memrealtime();
                     }
                     if (!ok && lane == 0) *sflag = 1;
                 }
@@ -325,6 +362,8 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
 #pragma unroll
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
+            if (a.ts && t == a.ts_step && threadIdx.x == 0)
+                atomicMin(a.ts + o * 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
             if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c)) return;
         }

@@ -54,6 +54,8 @@ _SIGS = {
     "lbc_team_events": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_team_ring": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_decode_path": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "lbc_one_stamps": ([_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
+                       ctypes.c_int),
     "lbc_team_stats": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_encode_ex": ([_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int, _P],

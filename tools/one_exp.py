@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Single-image decode experiment (k_dec_one, csrc/one.hip): one seeded 768x768 B8_lowrate frame encoded by the
+library, decoded through lbc_decode as one image -- k_dec_one -- and through the row graphs (LBIC_ONE=0), host clock
+around synchronize (eval_model's timing), median of REPS; then one decode with LBIC_ONE_STAMPS=1: per-operation stamps
+of the middle raster step.  Prints JSON lines."""
+import json
+import os
+import sys
+import time
+import types
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "learned-block-based-image-compression_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from lbic.arch import Arch  # noqa: E402
+from lbic.layout import image_to_blocks  # noqa: E402
+from lbic.model import BlockBasedImgCompLossyNetv9  # noqa: E402
+from lbic.weights import synth_state_dict  # noqa: E402
+
+OPS = ["ctx0", "ctx1", "ctx2", "ctx3", "rans", "dec0", "ig0", "d1", "ig1", "d2", "ig2", "d3"]
+
+
+def main():
+    size = int(os.environ.get("SIZE", "768"))
+    reps = int(os.environ.get("REPS", "3"))
+    arch = Arch(8, (3, 1, 1, 1), 768, 96)
+    cfg = types.SimpleNamespace(block_size=8, KS=[3, 1, 1, 1], N=768, M=96, gpu_device=0)
+    m = BlockBasedImgCompLossyNetv9(cfg)
+    m.load_state_dict(synth_state_dict(arch, 1337, rate="low"))
+    m.update(force=True)
+    img = np.random.default_rng(12345).integers(0, 256, (3, size, size), dtype=np.uint8).astype(np.float32) / 255 - 0.5
+    x = torch.from_numpy(image_to_blocks(img, 8))[None].cuda()
+    r = m.compress_batch(x)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    Hb = Wb = size // 8
+    for mode in ("1", "0"):
+        os.environ["LBIC_ONE"] = mode
+        ts = []
+        for k in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            z = m.decompress_batch(st, Hb, Wb)
+            torch.cuda.synchronize()
+            if k:
+                ts.append(time.time() - t0)
+        print(json.dumps(dict(decoder=m.decode_path()["path"], ms=round(float(np.median(ts)) * 1e3, 2),
+                              us_per_step=round(float(np.median(ts)) * 1e6 / (Hb * Wb), 2),
+                              bit_exact=bool(torch.equal(z, r["zhat"])))), flush=True)
+    os.environ["LBIC_ONE"] = "1"
+    os.environ["LBIC_ONE_STAMPS"] = "1"
+    z = m.decompress_batch(st, Hb, Wb)
+    os.environ["LBIC_ONE_STAMPS"] = "0"
+    s = m.one_stamps()
+    print(json.dumps(dict(stamps_us={OPS[o]: s[o] for o in range(len(s))}, bit_exact=bool(torch.equal(z, r["zhat"])))),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
