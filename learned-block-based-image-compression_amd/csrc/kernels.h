@@ -165,6 +165,8 @@ struct OneOp {
     int gx_src;              // GDN / IGDN: the op whose granules hold the layer input x
     unsigned long long* gran;   // this op's output granules [gw] {float bits, step + 1}
     int gw;                  // granule width (N padded to 16)
+    int sent_src, sent_idx, sent_dt;   // the sentinel granule: op sent_src's granule sent_idx at step tag + sent_dt
+                                       // (the op's latest input; -1: none)
 };
 struct OneArgs {
     const OneOp* ops;        // [nops] device, read-only for the launch
@@ -179,6 +181,7 @@ struct OneArgs {
     unsigned* fail;          // failure word (1: a wait timed out), zeroed before the launch
     unsigned long long tmo;  // s_memrealtime ticks one wait may take
     int lazy_z;              // 1 (Wb >= 3): a d3 producer drains its zpad store of step t only before publishing step t + 1
+    int sentinel;            // 1: one lane polls each op's sentinel granule before the waves load their inputs
     int ts_step;             // the sampled raster step of `ts`
     unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step: [0] first workgroup in, [1] last
                              // workgroup's partials reduced (inputs waited + chains), [2] last one published

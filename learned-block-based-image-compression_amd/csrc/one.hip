@@ -74,11 +74,10 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     for (;;) {
         bool ok = true;
         uint4 q[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int j = (p * 64 + lane) * 2;
-            q[p] = ld16_sc1(gran, (unsigned)(g0 + min(j, max(cnt - 2, 0))) * 8u);
-        }
+        // only the granules asked for (a poll is a memory-side round trip of every polling wave on the chip)
+        q[0] = q[1] = uint4{0u, 0u, 0u, 0u};
+        if (lane * 2 < cnt) q[0] = ld16_sc1(gran, (unsigned)(g0 + lane * 2) * 8u);
+        if (cnt > 128 && 128 + lane * 2 < cnt) q[1] = ld16_sc1(gran, (unsigned)(g0 + 128 + lane * 2) * 8u);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int j = (p * 64 + lane) * 2;
@@ -142,6 +141,28 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     bool ok = true;
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
+    // sentinel (a.sentinel): while the op's latest input is not there, ONE lane polls one granule of it (the others sit
+    // at the workgroup barrier) instead of every wave sweeping its whole slice -- a workgroup that reaches its next op
+    // early would otherwise load its whole input from the memory side once per round trip until it arrives
+    if (a.sentinel && op.sent_src >= 0 && !(op.sent_dt < 0 && (h == 0 || tag == 1))) {
+        if (threadIdx.x == 0) {
+            const OneOp& so = *(const OneOp*)((cop_p)a.ops + op.sent_src);
+            const unsigned want = tag + (unsigned)op.sent_dt;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                const unsigned long long w = __hip_atomic_load((gptr<unsigned long long>)(so.gran + op.sent_idx),
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)(w >> 32) == want) break;
+                if (__hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
+                    __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+    }
     // the epilogue operands of this op's tiles (bias: read-only), requested before anything waits
     float bb[ONE_NT_MAX];
 #pragma unroll
