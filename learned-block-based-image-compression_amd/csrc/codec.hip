@@ -1316,30 +1316,6 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
         }
         if (q.seg[q.nseg - 1].k1 != q.K) return LBC_OK;
     }
-    // sentinels: the latest input of each op -- a granule segment of this step (the highest source op), else the
-    // previous step's d3 through the left window tap
-    for (int o = 0; o < ONE_MAXOPS; ++o) {
-        OneOp& q = ops[o];
-        q.sent_src = -1;
-        q.sent_idx = 0;
-        q.sent_dt = 0;
-        if (o == 4) continue;
-        for (int i = 0; i < q.nseg; ++i) {
-            const OneSeg& sg = q.seg[i];
-            if (sg.kind == ONE_GRAN && sg.src > q.sent_src) {
-                q.sent_src = sg.src;
-                q.sent_idx = sg.c0 + sg.k1 - sg.k0 - 1;
-                q.sent_dt = 0;
-            }
-        }
-        if (q.sent_src < 0)
-            for (int i = 0; i < q.nseg; ++i)
-                if (q.seg[i].kind == ONE_ZTAP && q.seg[i].dy == 0 && q.seg[i].dx == -1) {
-                    q.sent_src = ONE_MAXOPS - 1;
-                    q.sent_idx = m->Cx - 1;
-                    q.sent_dt = -1;
-                }
-    }
     // granule buffers
     size_t ng = 0;
     for (const OneOp& q : ops) ng += (size_t)q.gw;
@@ -1403,9 +1379,9 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.fail = m->one_fail.as<unsigned>();
     a.tmo = 100000000ull;     // 1 s per wait (100 MHz)
     a.lazy_z = Wb >= 3 ? 1 : 0;
-    a.sentinel = 1;
+    a.rans_lds_tab = (size_t)m->total16 * 2 <= wmax * 16 && m->total16 % 8 == 0 ? 1 : 0;
     a.ts_step = (Hb / 2) * Wb + Wb / 2;
-    if ((rc = m->one_ts.alloc(ONE_MAXOPS * 4 * sizeof(unsigned long long)))) return rc;
+    if ((rc = m->one_ts.alloc((ONE_MAXOPS * 4 + 4) * sizeof(unsigned long long)))) return rc;
     if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4)) < 1) return LBC_OK;
     m->one_grid = G;
     m->one_ok = 1;
@@ -1425,9 +1401,8 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     if (!m->one_ok) return LBC_OK;
     OneArgs a = m->one_args;
     if (const char* t = getenv("LBIC_ONE_TMO")) a.tmo = std::max(1ull, strtoull(t, nullptr, 10));   // test hook
-    if (const char* se = getenv("LBIC_ONE_SENT")) a.sentinel = atoi(se) ? 1 : 0;   // A/B runs
     const char* st = getenv("LBIC_ONE_STAMPS");
-    std::vector<unsigned long long> ts0(ONE_MAXOPS * 4, 0ull);
+    std::vector<unsigned long long> ts0(ONE_MAXOPS * 4 + 4, 0ull);
     if (st && atoi(st)) {
         for (int o = 0; o < ONE_MAXOPS; ++o) ts0[o * 4] = ~0ull;
         HIPCHK(hipMemcpyAsync(m->one_ts.p, ts0.data(), ts0.size() * 8, hipMemcpyHostToDevice, s));
@@ -1437,8 +1412,8 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     HIPCHK(hipMemsetAsync(m->one_fail.p, 0, 64, s));
     if ((rc = launch_dec_one(a, m->one_grid, s))) return rc;
     if (a.ts) {
-        m->one_ts_host.assign(ONE_MAXOPS * 4, 0ull);
-        HIPCHK(hipMemcpyAsync(m->one_ts_host.data(), a.ts, ONE_MAXOPS * 4 * 8, hipMemcpyDeviceToHost, s));
+        m->one_ts_host.assign(ONE_MAXOPS * 4 + 4, 0ull);
+        HIPCHK(hipMemcpyAsync(m->one_ts_host.data(), a.ts, (ONE_MAXOPS * 4 + 4) * 8, hipMemcpyDeviceToHost, s));
     }
     unsigned fail = 0;
     HIPCHK(hipMemcpyAsync(&fail, m->one_fail.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));

@@ -165,8 +165,6 @@ struct OneOp {
     int gx_src;              // GDN / IGDN: the op whose granules hold the layer input x
     unsigned long long* gran;   // this op's output granules [gw] {float bits, step + 1}
     int gw;                  // granule width (N padded to 16)
-    int sent_src, sent_idx, sent_dt;   // the sentinel granule: op sent_src's granule sent_idx at step tag + sent_dt
-                                       // (the op's latest input; -1: none)
 };
 struct OneArgs {
     const OneOp* ops;        // [nops] device, read-only for the launch
@@ -181,10 +179,11 @@ struct OneArgs {
     unsigned* fail;          // failure word (1: a wait timed out), zeroed before the launch
     unsigned long long tmo;  // s_memrealtime ticks one wait may take
     int lazy_z;              // 1 (Wb >= 3): a d3 producer drains its zpad store of step t only before publishing step t + 1
-    int sentinel;            // 1: one lane polls each op's sentinel granule before the waves load their inputs
+    int rans_lds_tab;        // 1: the rANS workgroup copies the table image into its (weight-free) LDS
     int ts_step;             // the sampled raster step of `ts`
     unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step: [0] first workgroup in, [1] last
-                             // workgroup's partials reduced (inputs waited + chains), [2] last one published
+                             // workgroup's partials reduced (inputs waited + chains), [2] last one published; then
+                             // [ONE_MAXOPS * 4] the rANS op's scale indexes computed, [+ 1] its symbols decoded
 };
 size_t one_lds_bytes(int wlds_f4);
 int one_blocks_per_cu(size_t lds);

@@ -105,10 +105,14 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
 
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
-    int4 r = my[0];
+    int x = my[0].x, y = my[0].y, z = my[0].z;
 #pragma unroll
-    for (int j = 1; j < ONE_NT_MAX; ++j) r = i == j ? my[j] : r;
-    return r;
+    for (int j = 1; j < ONE_NT_MAX; ++j) {
+        x = i == j ? my[j].x : x;
+        y = i == j ? my[j].y : y;
+        z = i == j ? my[j].z : z;
+    }
+    return make_int4(x, y, z, 0);
 }
 
 __device__ __forceinline__ float pick_f(const float (&v)[ONE_NT_MAX], int i) {
@@ -141,29 +145,22 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     bool ok = true;
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
-    // sentinel (a.sentinel): while the op's latest input is not there, ONE lane polls one granule of it (the others sit
-    // at the workgroup barrier) instead of every wave sweeping its whole slice -- a workgroup that reaches its next op
-    // early would otherwise load its whole input from the memory side once per round trip until it arrives
-    if (a.sentinel && op.sent_src >= 0 && !(op.sent_dt < 0 && (h == 0 || tag == 1))) {
-        if (threadIdx.x == 0) {
-            const OneOp& so = *(const OneOp*)((cop_p)a.ops + op.sent_src);
-            const unsigned want = tag + (unsigned)op.sent_dt;
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                const unsigned long long w = __hip_atomic_load((gptr<unsigned long long>)(so.gran + op.sent_idx),
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((unsigned)(w >> 32) == want) break;
-                if (__hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
-                    __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __syncthreads();
+    // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
+#ifdef LBIC_ONE_WPRE   // (experiment build: the first tile's weight fragments in registers before the waits)
+    int i0 = ONE_NT_MAX - 1, z0 = my[ONE_NT_MAX - 1].z;
+#pragma unroll
+    for (int i = ONE_NT_MAX - 1; i >= 0; --i) {
+        const bool hit = my[i].x == o;
+        i0 = hit ? i : i0;
+        z0 = hit ? my[i].z : z0;
     }
-    // the epilogue operands of this op's tiles (bias: read-only), requested before anything waits
+    f4 wpre[LL];
+    {
+        const f4* wt = wl + z0 + lane;
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) wpre[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
+    }
+#endif
     float bb[ONE_NT_MAX];
 #pragma unroll
     for (int i = 0; i < ONE_NT_MAX; ++i) {
@@ -233,8 +230,16 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         const f4* wt = wl + ti.z + lane;
         f4 acc = f4{0.f, 0.f, 0.f, 0.f};
         f4 wv[LL];
+#ifdef LBIC_ONE_WPRE
+        if (i == i0) {
 #pragma unroll
-        for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
+            for (int cc = 0; cc < LL; ++cc) wv[cc] = wpre[cc];
+        } else
+#endif
+        {
+#pragma unroll
+            for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
+        }
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
             f4 t = acc;
@@ -285,14 +290,29 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     return good;
 }
 
+// LL = fragments per wave: L = (K / 16) / 8 k-blocks per slice, L + 1 when the slices differ in length (the extra
+// fragment's MFMAs are discarded), L when every slice has exactly L (nothing to discard: a shorter chain)
 __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v, int h,
                              unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c) {
-    switch ((op.K >> 4) / KSPLIT) {
+    const int nkb = op.K >> 4;
+    int key = (nkb / KSPLIT) * 2 + (nkb % KSPLIT == 0 ? 1 : 0);
+#ifndef LBIC_ONE_EXACT_ALL
+    if ((key & 1) && key != 13 && key != 19) key &= ~1;     // exact slices without an instance: the L + 1 form
+#endif
+    switch (key) {
 #define LBIC_ONE(L_) \
-    case L_: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
+    case L_ * 2: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
+#define LBIC_ONE_EX(L_) \
+    case L_ * 2 + 1: return one_gemm<L_>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
         LBIC_ONE(0) LBIC_ONE(1) LBIC_ONE(2) LBIC_ONE(3) LBIC_ONE(4) LBIC_ONE(5) LBIC_ONE(6) LBIC_ONE(7) LBIC_ONE(8)
         LBIC_ONE(9) LBIC_ONE(10) LBIC_ONE(11)
+#ifdef LBIC_ONE_EXACT_ALL
+        LBIC_ONE_EX(1) LBIC_ONE_EX(2) LBIC_ONE_EX(3) LBIC_ONE_EX(4) LBIC_ONE_EX(5) LBIC_ONE_EX(7) LBIC_ONE_EX(8)
+        LBIC_ONE_EX(10) LBIC_ONE_EX(11) LBIC_ONE_EX(12)
+#endif
+        LBIC_ONE_EX(6) LBIC_ONE_EX(9)   // K = 768, 1152 (the B8 context / decoder widths)
 #undef LBIC_ONE
+#undef LBIC_ONE_EX
         default: return false;   // (the host admits K <= 1536 only)
     }
 }
@@ -340,8 +360,17 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
         rcache[4] = 0u;    // no cached coder state yet
         *sflag = 0;
     }
-    __syncthreads();
     const RansArgs& R = *(const RansArgs*)((const __attribute__((address_space(4))) RansArgs*)a.rans);
+    // the stream's workgroup holds no weights: its LDS takes a copy of the table image, so the rare symbols off the
+    // centre intervals are searched in LDS instead of global memory (two dependent loads each)
+    const uint16_t* ltab = nullptr;
+    if (rank == a.rans_wg && a.rans_lds_tab) {
+        const uint4* src = reinterpret_cast<const uint4*>(R.cdf16);
+        uint4* dst = reinterpret_cast<uint4*>(wl);
+        for (int i = threadIdx.x; i < R.total16 / 8; i += blockDim.x) dst[i] = src[i];
+        ltab = reinterpret_cast<const uint16_t*>(wl);
+    }
+    __syncthreads();
     for (int t = 0; t < a.Hb * a.Wb; ++t) {
         const int v = t / a.Wb, h = t - v * a.Wb;
         const unsigned tag = (unsigned)t + 1u;
@@ -363,10 +392,12 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                     for (int i = lane; i < M; i += 64) l_idx[i] = scale_index(l_ksi[i], a.table);
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
+                    if (stamp) a.ts[ONE_MAXOPS * 4] = __builtin_amdgcn_s_memrealtime();
                     if (ok) {
-                        rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, nullptr, rcache, l_idx, l_ksi, l_yq);
+                        rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache, l_idx, l_ksi, l_yq);
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
+                        if (stamp) a.ts[ONE_MAXOPS * 4 + 1] = __builtin_amdgcn_s_memrealtime();
                         const OneOp& yo = *(const OneOp*)((cop_p)a.ops + o);
                         for (int i = lane; i < yo.gw; i += 64) st_gran(yo.gran + i, i < M ? l_yq[i] : 0.f, tag);
                         if (stamp) a.ts[o * 4 + 2] = __builtin_amdgcn_s_memrealtime();

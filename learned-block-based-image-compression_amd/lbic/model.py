@@ -269,15 +269,18 @@ class BlockBasedImgCompLossyNetv9:
     def one_stamps(self):
         """Per-operation stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (lbc_one_stamps): a list of
         [first in, last reduced, last published] in us relative to the first operation's first entry."""
-        arr = (ctypes.c_ulonglong * 48)()
+        arr = (ctypes.c_ulonglong * 52)()
         n = ctypes.c_int()
-        _lib.check(_lib.lib().lbc_one_stamps(self._h, arr, 48, ctypes.byref(n)))
+        _lib.check(_lib.lib().lbc_one_stamps(self._h, arr, 52, ctypes.byref(n)))
         v = list(arr[:n.value])
         if not v:
             return []
-        t0 = min(x for x in v[0::4] if x) if any(v[0::4]) else 0
-        return [[round((v[4 * o + k] - t0) / 100.0, 2) if v[4 * o + k] and v[4 * o + k] != 2 ** 64 - 1 else None
-                 for k in range(3)] for o in range(n.value // 4)]
+        t0 = min(x for x in v[0:48:4] if x) if any(v[0:48:4]) else 0
+        rel = lambda x: round((x - t0) / 100.0, 2) if x and x != 2 ** 64 - 1 else None
+        out = [[rel(v[4 * o + k]) for k in range(3)] for o in range(min(12, n.value // 4))]
+        if n.value >= 50:
+            out.append([rel(v[48]), rel(v[49])])     # the rANS op: scale indexes computed, symbols decoded
+        return out
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
         """RansDecoder.decode_with_indexes (net:439) on the GPU for n streams at once: indexes [C, n, M]

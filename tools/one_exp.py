@@ -20,7 +20,7 @@ from lbic.layout import image_to_blocks  # noqa: E402
 from lbic.model import BlockBasedImgCompLossyNetv9  # noqa: E402
 from lbic.weights import synth_state_dict  # noqa: E402
 
-OPS = ["ctx0", "ctx1", "ctx2", "ctx3", "rans", "dec0", "ig0", "d1", "ig1", "d2", "ig2", "d3"]
+OPS = ["ctx0", "ctx1", "ctx2", "ctx3", "rans", "dec0", "ig0", "d1", "ig1", "d2", "ig2", "d3", "rans_idx_coded"]
 
 
 def main():
