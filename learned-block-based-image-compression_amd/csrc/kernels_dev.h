@@ -101,10 +101,20 @@ __device__ unsigned long long* g_phase;
 
 __device__ __forceinline__ int scale_index(float s, const float* table) {
     // build_indexes (entropy_layers_cai.py:649-654): idx = 63 - #{k < 63 : max(s, .11) <= table[k]}
+    //   = #{k < 63 : table[k] < s} for an increasing table (the compares are the same float compares).
+    // The table is get_scale_table()'s geometric grid, so s's position on it (approximate: a log) leaves the count in a
+    // window of four entries, which exact compares settle; the two outer compares prove the window holds the count, and
+    // any other table (or a position off by more than one) takes the full count.  One round of 4 (L1-resident) loads
+    // instead of 63 loads in 8 rounds.
     s = fmaxf(s, 0.11f);
+    const float t0 = table[0], t62 = table[62];
+    const float u = __logf(s / t0) / __logf(t62 / t0) * 62.f;
+    const int k = (int)floorf(fminf(fmaxf(u, 0.f), 62.f));
+    const float tm = table[max(k - 1, 0)], tk = table[k], tp = table[min(k + 1, 62)], tq = table[min(k + 2, 62)];
+    if ((k == 0 || tm < s) && (k + 2 > 62 || !(tq < s))) return k + (tk < s ? 1 : 0) + (k + 1 <= 62 && tp < s ? 1 : 0);
     int idx = 63;
 #pragma unroll 8
-    for (int k = 0; k < 63; ++k) idx -= (s <= table[k]) ? 1 : 0;
+    for (int j = 0; j < 63; ++j) idx -= (s <= table[j]) ? 1 : 0;
     return idx;
 }
 
@@ -441,12 +451,14 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
     const int nw_in = a.word_count[img];
     // table of symbol i (ti) and of symbol i + 1 (tn: the next symbol's metadata is read a symbol ahead)
     int ti[4], tn[4];
+    float mv[4];         // the means, requested with the indexes (not after the decode: one round trip less per block)
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
         // clamped, unconditional loads (indexes are 0..63 by construction; entries past Mlat are unused)
         ti[kb] = ld<TEAM>(a.idx + (long)row * Mlat + min(i, Mlat - 1)) & 63;
         tn[kb] = ld<TEAM>(a.idx + (long)row * Mlat + min(i + 1, Mlat - 1)) & 63;
+        mv[kb] = a.sym_out ? 0.f : ld<TEAM>(a.ksi + (long)row * a.ldk + Mlat + min(i, Mlat - 1));
     }
     // LDS staging: the tables (one image built on the host) and this wave's stream words p0 .. p0 +
     // RANS_WIN - 1 (0 past the stream's end; a block never needs more: <= 52 bits per symbol incl. a
@@ -586,7 +598,7 @@ __device__ __forceinline__ void rans_row(const RansArgs& a, uint16_t* lds, int r
         const int i = kb * 64 + lane;
         if (i < Mlat) {
             if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
-            else st<TEAM>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + ld<TEAM>(a.ksi + (long)row * a.ldk + Mlat + i), wt);
+            else st<TEAM>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + mv[kb], wt);
         }
     }
     if (lane == 0) {
@@ -634,6 +646,19 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
         ti[kb] = (LOCAL ? lidx[min(kb * 64 + lane, Mlat - 1)] : ld<SC1>(a.idx + (long)row * Mlat + min(kb * 64 + lane, Mlat - 1))) & 63;
+    // the means (y_qnt = symbol + mean) requested with the indexes, not after the decode: the context net wrote both
+    // in the same epilogue, and a load issued at the end would add a memory round trip to every block
+    float mv[4];
+    if (LOCAL || !a.sym_out) {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            const int i = min(kb * 64 + lane, Mlat - 1);
+            mv[kb] = LOCAL ? lksi[Mlat + i] : ld<SC1>(a.ksi + (long)row * a.ldk + Mlat + i);
+        }
+    } else {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) mv[kb] = 0.f;
+    }
     int t_fb, t_S, t_lm2, t_ca, t_off, t_lf, t_lfm, t_lfp;
     unsigned long long x;
     int p, nw, p0;
@@ -677,6 +702,10 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     int lov[4], frv[4], ivm[4], ivp[4], sfb[4], sS[4], slm[4], sca[4], moff[4], symv[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
+        if (kb * 64 >= Mlat) {           // (uniform) no symbols in this chunk: skip its nine gathers
+            lov[kb] = frv[kb] = ivm[kb] = ivp[kb] = sfb[kb] = sS[kb] = slm[kb] = sca[kb] = moff[kb] = symv[kb] = 0;
+            continue;
+        }
         const int sel = ti[kb] << 2;
         const int lf = __builtin_amdgcn_ds_bpermute(sel, t_lf);
         lov[kb] = lf & 0xffff;
@@ -840,9 +869,9 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     for (int kb = 0; kb < 4; ++kb) {
         const int i = kb * 64 + lane;
         if (i < Mlat) {
-            if constexpr (LOCAL) lyq[i] = (float)(symv[kb] + moff[kb]) + lksi[Mlat + i];
+            if constexpr (LOCAL) lyq[i] = (float)(symv[kb] + moff[kb]) + mv[kb];
             else if (a.sym_out) a.sym_out[(long)row * Mlat + i] = symv[kb] + moff[kb];
-            else st<SC1>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + ld<SC1>(a.ksi + (long)row * a.ldk + Mlat + i), wt);
+            else st<SC1>(a.yq + (long)row * a.ldy + i, (float)(symv[kb] + moff[kb]) + mv[kb], wt);
         }
     }
     if (lane == 0) {

@@ -71,7 +71,7 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
                                                const OneCtl& c, bool ge = false) {
     const int lane = threadIdx.x & 63;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
+    for (int it = 0;; ++it) {
         bool ok = true;
         uint4 q[2];
         // only the granules asked for (a poll is a memory-side round trip of every polling wave on the chip)
@@ -94,7 +94,10 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
             }
             return true;
         }
-        if (__hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        // the failure word only every 16th poll: a poll is one memory round trip, not two
+        if ((it & 15) == 15 &&
+            __hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return false;
         if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
             if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
@@ -146,21 +149,6 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
     // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
-#ifdef LBIC_ONE_WPRE   // (experiment build: the first tile's weight fragments in registers before the waits)
-    int i0 = ONE_NT_MAX - 1, z0 = my[ONE_NT_MAX - 1].z;
-#pragma unroll
-    for (int i = ONE_NT_MAX - 1; i >= 0; --i) {
-        const bool hit = my[i].x == o;
-        i0 = hit ? i : i0;
-        z0 = hit ? my[i].z : z0;
-    }
-    f4 wpre[LL];
-    {
-        const f4* wt = wl + z0 + lane;
-#pragma unroll
-        for (int cc = 0; cc < LL; ++cc) wpre[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
-    }
-#endif
     float bb[ONE_NT_MAX];
 #pragma unroll
     for (int i = 0; i < ONE_NT_MAX; ++i) {
@@ -230,16 +218,8 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         const f4* wt = wl + ti.z + lane;
         f4 acc = f4{0.f, 0.f, 0.f, 0.f};
         f4 wv[LL];
-#ifdef LBIC_ONE_WPRE
-        if (i == i0) {
 #pragma unroll
-            for (int cc = 0; cc < LL; ++cc) wv[cc] = wpre[cc];
-        } else
-#endif
-        {
-#pragma unroll
-            for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
-        }
+        for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
             f4 t = acc;

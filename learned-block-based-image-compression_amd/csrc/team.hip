@@ -497,8 +497,9 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
     if (threadIdx.x == 0) {
         int f = 0;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        // the failure word only every 16th poll: each poll is then one round trip to the team's L2, not two
+        for (int it = 0; __hip_atomic_load((gptr<unsigned>)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
+            if ((it & 15) == 15 && __hip_atomic_load((gptr<unsigned>)fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 f = 1;
                 break;
             }
