@@ -149,7 +149,8 @@ int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, 
 int lbc_decode_path(const lbc_model *m, int *path, int *timeouts);
 /* raw stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (diagnostic): 4 per operation of the raster step
  * (Hb/2, Wb/2), s_memrealtime (100 MHz): [0] first workgroup entering the operation, [1] the last one's partials
- * reduced (inputs waited for, chains done), [2] the last one's outputs published. */
+ * reduced (inputs waited for, chains done), [2] the last one's outputs published, [3] the last one's inputs all there;
+ * then [48] the rANS operation's scale indexes computed, [49] its symbols decoded. */
 int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 
 /* decompress() of n_teams batches at once (reference format; no reference counterpart for the batching: the

@@ -182,7 +182,8 @@ struct OneArgs {
     int rans_lds_tab;        // 1: the rANS workgroup copies the table image into its (weight-free) LDS
     int ts_step;             // the sampled raster step of `ts`
     unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step: [0] first workgroup in, [1] last
-                             // workgroup's partials reduced (inputs waited + chains), [2] last one published; then
+                             // workgroup's partials reduced (inputs waited + chains), [2] last one published, [3] the
+                             // last workgroup's inputs all there (GEMMs; an extra barrier in stamped steps); then
                              // [ONE_MAXOPS * 4] the rANS op's scale indexes computed, [+ 1] its symbols decoded
 };
 size_t one_lds_bytes(int wlds_f4);

@@ -184,6 +184,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
             ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), zneed, scr + 240, c, true);
     }
+    if (a.ts && t == a.ts_step) {     // (stamps only: every wave's inputs are there)
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(a.ts + o * 4 + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
     __builtin_amdgcn_wave_barrier();
@@ -225,7 +229,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             f4 t = acc;
 #pragma unroll
             for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cc][e], wv[cc][e], t, 0, 0, 0);
-            acc = cc < n ? t : acc;
+            acc = (cc < LL - 1 || cc < n) ? t : acc;    // n >= LL - 1: only the last fragment can be discarded
         }
         if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
         __syncthreads();

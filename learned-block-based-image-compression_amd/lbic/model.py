@@ -268,7 +268,8 @@ class BlockBasedImgCompLossyNetv9:
 
     def one_stamps(self):
         """Per-operation stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (lbc_one_stamps): a list of
-        [first in, last reduced, last published] in us relative to the first operation's first entry."""
+        [first in, last inputs there, last reduced, last published] in us relative to the first operation's first entry
+        (then [scale indexes done, symbols decoded] of the rANS operation)."""
         arr = (ctypes.c_ulonglong * 52)()
         n = ctypes.c_int()
         _lib.check(_lib.lib().lbc_one_stamps(self._h, arr, 52, ctypes.byref(n)))
@@ -277,7 +278,7 @@ class BlockBasedImgCompLossyNetv9:
             return []
         t0 = min(x for x in v[0:48:4] if x) if any(v[0:48:4]) else 0
         rel = lambda x: round((x - t0) / 100.0, 2) if x and x != 2 ** 64 - 1 else None
-        out = [[rel(v[4 * o + k]) for k in range(3)] for o in range(min(12, n.value // 4))]
+        out = [[rel(v[4 * o + k]) for k in (0, 3, 1, 2)] for o in range(min(12, n.value // 4))]
         if n.value >= 50:
             out.append([rel(v[48]), rel(v[49])])     # the rANS op: scale indexes computed, symbols decoded
         return out
