@@ -1381,7 +1381,7 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.lazy_z = Wb >= 3 ? 1 : 0;
     a.rans_lds_tab = (size_t)m->total16 * 2 <= wmax * 16 && m->total16 % 8 == 0 ? 1 : 0;
     a.ts_step = (Hb / 2) * Wb + Wb / 2;
-    if ((rc = m->one_ts.alloc((ONE_MAXOPS * 4 + 4) * sizeof(unsigned long long)))) return rc;
+    if ((rc = m->one_ts.alloc(ONE_TS_WORDS * sizeof(unsigned long long)))) return rc;
     if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4)) < 1) return LBC_OK;
     m->one_grid = G;
     m->one_ok = 1;
@@ -1402,7 +1402,7 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     OneArgs a = m->one_args;
     if (const char* t = getenv("LBIC_ONE_TMO")) a.tmo = std::max(1ull, strtoull(t, nullptr, 10));   // test hook
     const char* st = getenv("LBIC_ONE_STAMPS");
-    std::vector<unsigned long long> ts0(ONE_MAXOPS * 4 + 4, 0ull);
+    std::vector<unsigned long long> ts0(ONE_TS_WORDS, 0ull);
     if (st && atoi(st)) {
         for (int o = 0; o < ONE_MAXOPS; ++o) ts0[o * 4] = ~0ull;
         HIPCHK(hipMemcpyAsync(m->one_ts.p, ts0.data(), ts0.size() * 8, hipMemcpyHostToDevice, s));
@@ -1412,8 +1412,8 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     HIPCHK(hipMemsetAsync(m->one_fail.p, 0, 64, s));
     if ((rc = launch_dec_one(a, m->one_grid, s))) return rc;
     if (a.ts) {
-        m->one_ts_host.assign(ONE_MAXOPS * 4 + 4, 0ull);
-        HIPCHK(hipMemcpyAsync(m->one_ts_host.data(), a.ts, (ONE_MAXOPS * 4 + 4) * 8, hipMemcpyDeviceToHost, s));
+        m->one_ts_host.assign(ONE_TS_WORDS, 0ull);
+        HIPCHK(hipMemcpyAsync(m->one_ts_host.data(), a.ts, ONE_TS_WORDS * 8, hipMemcpyDeviceToHost, s));
     }
     unsigned fail = 0;
     HIPCHK(hipMemcpyAsync(&fail, m->one_fail.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));

@@ -130,11 +130,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
 // differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
 // selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
-// MINL: n >= LL - 1 (a slice of L or L + 1 k-blocks): only the last fragment's MFMAs can be discarded, so the chain's
-// other steps feed the next MFMA directly (a select between two dependent MFMAs costs the chain its forwarding: an
-// s_nop for the MFMA's latency, four v_cndmask and another s_nop per k-block).  The long-K chunks (n of 1..12) select
-// at every step.
-template <int L, bool RASTER, bool EXACT = false, bool MINL = true>
+template <int L, bool RASTER, bool EXACT = false>
 __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int nt, int m0, int lane, const BlkSrc& blocks,
                                           f4 acc) {
     constexpr int LL = EXACT ? L : L + 1;     // EXACT: every slice has exactly L k-blocks (K/16 divisible by 8)
@@ -174,7 +170,7 @@ __device__ __forceinline__ f4 small_slice(const GemmArgs& g, int kb0, int n, int
         f4 t = acc;
 #pragma unroll
         for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-        acc = ((MINL && c < LL - 1) || c < n) ? t : acc;
+        acc = c < n ? t : acc;
     }
     return acc;
 }
@@ -215,7 +211,7 @@ __global__ __launch_bounds__(512) void k_gemm_s(const GemmArgs g) {
         acc = small_slice<L, RASTER, EXACT>(g, kb0, kb1 - kb0, nt, m0, lane, blocks, acc);
     } else {
         for (int c0 = kb0; c0 < kb1; c0 += 12)
-            acc = small_slice<11, RASTER, false, false>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
+            acc = small_slice<11, RASTER>(g, c0, min(12, kb1 - c0), nt, m0, lane, blocks, acc);
     }
     PHASE(3);
     DPH(2);

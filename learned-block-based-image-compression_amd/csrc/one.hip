@@ -148,6 +148,14 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     bool ok = true;
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
+    // (stamps only) this workgroup holds column tile 0 of the op: its wave 0 stamps the phases of the step
+    bool dg = false;
+    if (a.ts && t == a.ts_step) {
+#pragma unroll
+        for (int i = 0; i < ONE_NT_MAX; ++i) dg |= my[i].x == o && my[i].y == 0;
+    }
+    unsigned long long* dts = a.ts + ONE_TS_DETAIL + o * 8;
+    if (dg && threadIdx.x == 0) dts[0] = __builtin_amdgcn_s_memrealtime();
     // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
     float bb[ONE_NT_MAX];
 #pragma unroll
@@ -162,6 +170,14 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     //  * the taps of the row above: zpad, visible once d3's granules have reached the producing step t' (+ 1, or + 2
     //    with lazy drains: a d3 producer drains its zpad store of step t' only before publishing step t' + 1)
     unsigned zneed = 0;
+    // (uniform) the common shape: the whole of K is one granule segment of one source op from its column c0
+    const bool gran1 = op.nseg == 1 && op.seg[0].kind == ONE_GRAN;
+    if (gran1) {
+        if (n > 0) {
+            const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
+            ok = wave_wait_gran(src.gran, op.seg[0].c0 + (kb0 << 4), n * 16, tag, scr, c);
+        }
+    } else
     for (int cb = 0; cb < n && ok;) {
         const int s = seg_of(op, kb0 + cb);
         const OneSeg& sg = op.seg[s];
@@ -187,6 +203,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     if (a.ts && t == a.ts_step) {     // (stamps only: every wave's inputs are there)
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(a.ts + o * 4 + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (dg && threadIdx.x == 0) {
+            dts[1] = __builtin_amdgcn_s_memrealtime();
+            dts[6] = __builtin_amdgcn_s_memtime();
+        }
     }
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
@@ -195,6 +215,16 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     const bool row0 = (lane & 15) == 0;
     const int q4 = (lane >> 4) * 4;
     const long cell = ((long)(v + 2) * a.Wp + (h + 2));
+    if (gran1) {      // every fragment from the wave's scratch: no per-k-block segment lookup
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) {
+            const int ci = max(min(cc, n - 1), 0);
+            f4 x = *reinterpret_cast<const f4*>(scr + ci * 16 + q4);
+            x = row0 ? x : f4{0.f, 0.f, 0.f, 0.f};
+            if (op.sq) x = x * x;
+            av[cc] = x;
+        }
+    } else
 #pragma unroll
     for (int cc = 0; cc < LL; ++cc) {
         const int ci = max(min(cc, n - 1), 0);      // (an empty slice, n = 0, loads k-block kb0 and adds nothing)
@@ -224,6 +254,11 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         f4 wv[LL];
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
+        const bool dgt = dg && nt == 0 && threadIdx.x == 0;
+        if (dgt) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            dts[2] = __builtin_amdgcn_s_memrealtime();
+        }
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
             f4 t = acc;
@@ -232,7 +267,9 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             acc = (cc < LL - 1 || cc < n) ? t : acc;    // n >= LL - 1: only the last fragment can be discarded
         }
         if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
+        if (dgt) dts[3] = __builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1 : 0);   // (after the chain's result)
         __syncthreads();
+        if (dgt) dts[4] = __builtin_amdgcn_s_memrealtime();
         if (a.ts && t == a.ts_step && threadIdx.x == 0)
             atomicMax(a.ts + o * 4 + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (threadIdx.x < 16) {
@@ -266,6 +303,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     }
     if (a.ts && t == a.ts_step && threadIdx.x == 0)
         atomicMax(a.ts + o * 4 + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (dg && threadIdx.x == 0) {
+        dts[5] = __builtin_amdgcn_s_memrealtime();
+        dts[7] = __builtin_amdgcn_s_memtime();
+    }
     // a uniform verdict for the whole workgroup
     if (!ok && lane == 0) *sflag = 1;
     __syncthreads();
@@ -376,12 +417,18 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                     for (int i = lane; i < M; i += 64) l_idx[i] = scale_index(l_ksi[i], a.table);
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
-                    if (stamp) a.ts[ONE_MAXOPS * 4] = __builtin_amdgcn_s_memrealtime();
+                    if (stamp) {
+                        a.ts[ONE_MAXOPS * 4] = __builtin_amdgcn_s_memrealtime();
+                        a.ts[ONE_MAXOPS * 4 + 2] = __builtin_amdgcn_s_memtime();    // (the shader clock: see below)
+                    }
                     if (ok) {
                         rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache, l_idx, l_ksi, l_yq);
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
-                        if (stamp) a.ts[ONE_MAXOPS * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+                        if (stamp) {
+                            a.ts[ONE_MAXOPS * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+                            a.ts[ONE_MAXOPS * 4 + 3] = __builtin_amdgcn_s_memtime();
+                        }
                         const OneOp& yo = *(const OneOp*)((cop_p)a.ops + o);
                         for (int i = lane; i < yo.gw; i += 64) st_gran(yo.gran + i, i < M ? l_yq[i] : 0.f, tag);
                         if (stamp) a.ts[o * 4 + 2] = __builtin_amdgcn_s_memrealtime();

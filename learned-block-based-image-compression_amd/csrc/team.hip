@@ -390,7 +390,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
                 f4 t = acc;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
-                acc = (c < LL - 1 || c < n) ? t : acc;   // n >= LL - 1: no select between dependent MFMAs
+                acc = c < n ? t : acc;
             }
             // partials -> LDS [item][slice][256]
 #pragma unroll

@@ -56,6 +56,9 @@ def main():
     s = m.one_stamps()
     print(json.dumps(dict(stamps_us={OPS[o]: s[o] for o in range(len(s))}, bit_exact=bool(torch.equal(z, r["zhat"])))),
           flush=True)
+    d = m.one_phase_stamps()
+    print(json.dumps(dict(phases_us={OPS[o]: d[o] for o in range(len(d)) if o != 4},
+                          keys=["in", "ready", "regs", "chain", "reduced", "published", "clk_MHz"])), flush=True)
 
 
 if __name__ == "__main__":
