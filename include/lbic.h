@@ -150,10 +150,10 @@ int lbc_decode_path(const lbc_model *m, int *path, int *timeouts);
 /* raw stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (diagnostic): 4 per operation of the raster step
  * (Hb/2, Wb/2), s_memrealtime (100 MHz): [0] first workgroup entering the operation, [1] the last one's partials
  * reduced (inputs waited for, chains done), [2] the last one's outputs published, [3] the last one's inputs all there;
- * then [48] the rANS operation's scale indexes computed, [49] its symbols decoded, [50], [51] s_memtime (shader clock)
- * at those two points; then 8 per operation from the workgroup holding its column tile 0 (wave 0): [52 + 8 o] in,
- * [+1] inputs there, [+2] A and weights in registers, [+3] chain done, [+4] partials reduced, [+5] published,
- * [+6], [+7] s_memtime at [+1] and [+5] (148 words). */
+ * then [48] the rANS operation's decode started, [49] its symbols decoded, [50], [51] s_memtime (shader clock)
+ * at those two points; then 8 per operation from the workgroup holding its column tile 0: [52 + 8 o] in, [+1] the last
+ * wave's inputs there, [+2] its A and weights in registers, [+3] its chain done, [+4] partials reduced, [+5] published,
+ * [+6] the first wave's inputs there, [+7] unused (148 words). */
 int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 
 /* decompress() of n_teams batches at once (reference format; no reference counterpart for the batching: the

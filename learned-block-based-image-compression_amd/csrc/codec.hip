@@ -1404,7 +1404,7 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     const char* st = getenv("LBIC_ONE_STAMPS");
     std::vector<unsigned long long> ts0(ONE_TS_WORDS, 0ull);
     if (st && atoi(st)) {
-        for (int o = 0; o < ONE_MAXOPS; ++o) ts0[o * 4] = ~0ull;
+        for (int o = 0; o < ONE_MAXOPS; ++o) ts0[o * 4] = ts0[ONE_TS_DETAIL + o * 8 + 6] = ~0ull;
         HIPCHK(hipMemcpyAsync(m->one_ts.p, ts0.data(), ts0.size() * 8, hipMemcpyHostToDevice, s));
         a.ts = m->one_ts.as<unsigned long long>();
     }

@@ -183,12 +183,12 @@ struct OneArgs {
     int ts_step;             // the sampled raster step of `ts`
     unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step: [0] first workgroup in, [1] last
                              // workgroup's partials reduced (inputs waited + chains), [2] last one published, [3] the
-                             // last workgroup's inputs all there (GEMMs; an extra barrier in stamped steps); then
-                             // [ONE_MAXOPS * 4] the rANS op's scale indexes computed, [+ 1] its symbols decoded,
+                             // last wave's inputs all there (GEMMs; per-wave stamps, no barrier); then
+                             // [ONE_MAXOPS * 4] the rANS op's decode started (inputs in LDS), [+ 1] its symbols decoded,
                              // [+ 2], [+ 3] s_memtime (shader clock) at those two points; then [ONE_TS_DETAIL + 8 o]
-                             // the workgroup holding column tile 0 of op o, wave 0: [0] in, [1] inputs there (its
-                             // barrier), [2] A and weights in registers, [3] chain done, [4] partials reduced, [5]
-                             // published (s_memrealtime), [6], [7] s_memtime at [1] and [5]
+                             // the workgroup holding column tile 0 of op o: [0] in, [1] the last wave's inputs there,
+                             // [2] its A and weights in registers, [3] its chain done, [4] partials reduced, [5]
+                             // published, [6] the first wave's inputs there, [7] unused
 };
 constexpr int ONE_TS_DETAIL = ONE_MAXOPS * 4 + 4;
 constexpr int ONE_TS_WORDS = ONE_TS_DETAIL + ONE_MAXOPS * 8;

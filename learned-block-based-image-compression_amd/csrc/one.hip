@@ -54,7 +54,7 @@ __device__ __forceinline__ float one_epi(int epi, float v, float b, float xv) {
         }
         case EPI_CLAMPZ:
             return fminf(fmaxf(v + b, -0.5f), 0.5f);
-        default:   // EPI_BIAS, EPI_CTXIDX (the value; the rANS workgroup derives the scale index itself)
+        default:   // EPI_BIAS, EPI_CTXIDX (the value; the caller turns the scale columns into scale indexes)
             return v + b;
     }
 }
@@ -200,12 +200,12 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
             ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), zneed, scr + 240, c, true);
     }
-    if (a.ts && t == a.ts_step) {     // (stamps only: every wave's inputs are there)
-        __syncthreads();
-        if (threadIdx.x == 0) atomicMax(a.ts + o * 4 + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        if (dg && threadIdx.x == 0) {
-            dts[1] = __builtin_amdgcn_s_memrealtime();
-            dts[6] = __builtin_amdgcn_s_memtime();
+    if (a.ts && t == a.ts_step && lane == 0) {     // (stamps only, no barrier: this wave's inputs are there)
+        const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+        atomicMax(a.ts + o * 4 + 3, r);
+        if (dg) {
+            atomicMax(dts + 1, r);
+            atomicMin(dts + 6, r);
         }
     }
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
@@ -254,10 +254,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         f4 wv[LL];
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
-        const bool dgt = dg && nt == 0 && threadIdx.x == 0;
+        const bool dgt = dg && nt == 0 && lane == 0;
         if (dgt) {
             __builtin_amdgcn_s_waitcnt(0xC07F);
-            dts[2] = __builtin_amdgcn_s_memrealtime();
+            atomicMax(dts + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
         }
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
@@ -267,9 +267,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             acc = (cc < LL - 1 || cc < n) ? t : acc;    // n >= LL - 1: only the last fragment can be discarded
         }
         if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
-        if (dgt) dts[3] = __builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1 : 0);   // (after the chain's result)
+        if (dgt)    // (after the chain's result)
+            atomicMax(dts + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1 : 0));
         __syncthreads();
-        if (dgt) dts[4] = __builtin_amdgcn_s_memrealtime();
+        if (dgt && threadIdx.x == 0) dts[4] = __builtin_amdgcn_s_memrealtime();
         if (a.ts && t == a.ts_step && threadIdx.x == 0)
             atomicMax(a.ts + o * 4 + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (threadIdx.x < 16) {
@@ -297,16 +298,16 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
                     if (!a.lazy_z) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tap data before the granule
                 }
             }
+            // the context net's scale columns go out as their scale indexes (build_indexes, the int in the float's
+            // bits): the rANS workgroup decodes from them directly, the search done here by 16 lanes per tile
+            if (op.epi == EPI_CTXIDX && col < a.Mlat) out = __int_as_float(scale_index(out, a.table));
             if (col < gw) st_gran(op.gran + col, out, tag);
         }
         __syncthreads();
     }
     if (a.ts && t == a.ts_step && threadIdx.x == 0)
         atomicMax(a.ts + o * 4 + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    if (dg && threadIdx.x == 0) {
-        dts[5] = __builtin_amdgcn_s_memrealtime();
-        dts[7] = __builtin_amdgcn_s_memtime();
-    }
+    if (dg && threadIdx.x == 0) dts[5] = __builtin_amdgcn_s_memrealtime();
     // a uniform verdict for the whole workgroup
     if (!ok && lane == 0) *sflag = 1;
     __syncthreads();
@@ -345,10 +346,10 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 }  // namespace
 
 // dynamic LDS: [weight tiles wlds_f4 float4s][partials KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
-// [rANS state cache ONE_RC_WORDS][idx 256][ksi 512][yq 256][flag 4 words]
+// [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words]
 size_t one_lds_bytes(int wlds_f4) {
     return (size_t)wlds_f4 * 16 + (size_t)(KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
-           (size_t)(RANS_WIN + ONE_RC_WORDS + 256 + 512 + 256 + 4) * 4;
+           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4;
 }
 
 __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
@@ -358,8 +359,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     float* scr = red + KSPLIT * 16;
     uint32_t* lwin = reinterpret_cast<uint32_t*>(scr + KSPLIT * ONE_SCR);
     uint32_t* rcache = lwin + RANS_WIN;
-    int32_t* l_idx = reinterpret_cast<int32_t*>(rcache + ONE_RC_WORDS);
-    float* l_ksi = reinterpret_cast<float*>(l_idx + 256);
+    float* l_ksi = reinterpret_cast<float*>(rcache + ONE_RC_WORDS);
     float* l_yq = l_ksi + 512;
     int* sflag = reinterpret_cast<int*>(l_yq + 256);
     const int rank = blockIdx.x;
@@ -406,7 +406,8 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                 const bool stamp = a.ts && t == a.ts_step && threadIdx.x == 0;
                 if (stamp) a.ts[o * 4] = __builtin_amdgcn_s_memrealtime();
                 if (wave == 0) {
-                    // scales | means of the context net (2 Mlat granules), scale indexes (build_indexes) into LDS
+                    // scale indexes | means of the context net (2 Mlat granules: ctx3's epilogue turned the scales into
+                    // their indexes) into LDS
                     const OneOp& ctx = *(const OneOp*)((cop_p)a.ops + (o - 1));
                     const int M = a.Mlat;
                     for (int g0 = 0; g0 < 2 * M && ok; g0 += 256)
@@ -414,15 +415,13 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
                     if (stamp) a.ts[o * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-                    for (int i = lane; i < M; i += 64) l_idx[i] = scale_index(l_ksi[i], a.table);
-                    __builtin_amdgcn_s_waitcnt(0xC07F);
-                    __builtin_amdgcn_wave_barrier();
                     if (stamp) {
                         a.ts[ONE_MAXOPS * 4] = __builtin_amdgcn_s_memrealtime();
                         a.ts[ONE_MAXOPS * 4 + 2] = __builtin_amdgcn_s_memtime();    // (the shader clock: see below)
                     }
                     if (ok) {
-                        rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache, l_idx, l_ksi, l_yq);
+                        rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache,
+                                                           reinterpret_cast<const int32_t*>(l_ksi), l_ksi, l_yq);
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
                         if (stamp) {

@@ -269,7 +269,7 @@ class BlockBasedImgCompLossyNetv9:
     def one_stamps(self):
         """Per-operation stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (lbc_one_stamps): a list of
         [first in, last inputs there, last reduced, last published] in us relative to the first operation's first entry
-        (then [scale indexes done, symbols decoded] of the rANS operation)."""
+        (then [decode started, symbols decoded, shader clock MHz] of the rANS operation)."""
         arr = (ctypes.c_ulonglong * 52)()
         n = ctypes.c_int()
         _lib.check(_lib.lib().lbc_one_stamps(self._h, arr, 52, ctypes.byref(n)))
@@ -280,7 +280,7 @@ class BlockBasedImgCompLossyNetv9:
         rel = lambda x: round((x - t0) / 100.0, 2) if x and x != 2 ** 64 - 1 else None
         out = [[rel(v[4 * o + k]) for k in (0, 3, 1, 2)] for o in range(min(12, n.value // 4))]
         if n.value >= 52:
-            # the rANS op: scale indexes computed, symbols decoded, and the shader clock over that span (MHz:
+            # the rANS op: decode started (inputs in LDS), symbols decoded, and the shader clock over that span (MHz:
             # s_memtime ticks / s_memrealtime ticks x 100 MHz)
             clk = round((v[51] - v[50]) / (v[49] - v[48]) * 100.0, 1) if v[49] > v[48] and v[51] > v[50] else None
             out.append([rel(v[48]), rel(v[49]), clk])
@@ -288,9 +288,9 @@ class BlockBasedImgCompLossyNetv9:
 
     def one_phase_stamps(self):
         """The phases of the sampled raster step in the workgroup holding column tile 0 of each GEMM operation (the
-        same launch as one_stamps): per op [in, inputs there, A and weights in registers, chain done, partials reduced,
-        published] in us relative to the first operation's first entry, then the shader clock in MHz over
-        inputs-there .. published (None for the rANS op)."""
+        same launch as one_stamps): per op [in, first wave's inputs there, last wave's inputs there, its A and weights
+        in registers, its chain done, partials reduced, published] in us relative to the first operation's first entry
+        (Nones for the rANS op)."""
         words = 52 + 12 * 8
         arr = (ctypes.c_ulonglong * words)()
         n = ctypes.c_int()
@@ -303,8 +303,7 @@ class BlockBasedImgCompLossyNetv9:
         out = []
         for o in range(12):
             d = v[52 + 8 * o: 60 + 8 * o]
-            clk = round((d[7] - d[6]) / (d[5] - d[1]) * 100.0, 1) if d[5] > d[1] and d[7] > d[6] else None
-            out.append([rel(x) for x in d[:6]] + [clk])
+            out.append([rel(d[k]) for k in (0, 6, 1, 2, 3, 4, 5)])
         return out
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
