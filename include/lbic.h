@@ -151,9 +151,9 @@ int lbc_decode_path(const lbc_model *m, int *path, int *timeouts);
  * (Hb/2, Wb/2), s_memrealtime (100 MHz): [0] first workgroup entering the operation, [1] the last one's partials
  * reduced (inputs waited for, chains done), [2] the last one's outputs published, [3] the last one's inputs all there;
  * then [48] the rANS operation's decode started, [49] its symbols decoded, [50], [51] s_memtime (shader clock)
- * at those two points; then 8 per operation from the workgroup holding its column tile 0: [52 + 8 o] in, [+1] the last
- * wave's inputs there, [+2] its A and weights in registers, [+3] its chain done, [+4] partials reduced, [+5] published,
- * [+6] the first wave's inputs there, [+7] unused (148 words). */
+ * at those two points; then 32 per operation from the workgroup holding its column tile 0: [52 + 32 o] in, [+1 + w]
+ * wave w's inputs there, [+9 + w] its A and weights in registers, [+17 + w] its chain done, [+25] partials reduced,
+ * [+26] published (436 words; every stamp is written after the operation's publish). */
 int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 
 /* decompress() of n_teams batches at once (reference format; no reference counterpart for the batching: the

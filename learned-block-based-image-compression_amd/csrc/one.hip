@@ -106,6 +106,22 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     }
 }
 
+// The gate of a far waiter: until the operation two before `o` (in raster-step order) has published its first granule,
+// the inputs of `o` cannot be complete; watching that one granule (one lane per wave) keeps the 64-lane polls of
+// workgroups that wait far ahead of the chain off the memory side, and leaves them at least one operation of slack to
+// start polling before their inputs land.
+__device__ __forceinline__ void one_gate(const OneArgs& a, int o, unsigned tag, float* scr, const OneCtl& c) {
+    int so = o - 2;
+    unsigned st = tag;
+    if (so < 0) {
+        so += a.nops;
+        st -= 1u;
+    }
+    if (st == 0u) return;
+    const OneOp& s = *(const OneOp*)((cop_p)a.ops + so);
+    (void)wave_wait_gran(s.gran, 0, 1, st, scr, c, true);
+}
+
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     int x = my[0].x, y = my[0].y, z = my[0].z;
@@ -148,14 +164,17 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     bool ok = true;
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
-    // (stamps only) this workgroup holds column tile 0 of the op: its wave 0 stamps the phases of the step
+    // (stamps only, step ts_step) times kept in registers and written after the publish, so that no stamp store or
+    // atomic sits in the memory queue the op's own waits drain; dg: this workgroup holds column tile 0 of the op and
+    // also records every wave's phases
+    const bool st_on = a.ts && t == a.ts_step;
     bool dg = false;
-    if (a.ts && t == a.ts_step) {
+    if (st_on) {
 #pragma unroll
         for (int i = 0; i < ONE_NT_MAX; ++i) dg |= my[i].x == o && my[i].y == 0;
     }
-    unsigned long long* dts = a.ts + ONE_TS_DETAIL + o * 8;
-    if (dg && threadIdx.x == 0) dts[0] = __builtin_amdgcn_s_memrealtime();
+    unsigned long long s_in = 0, s_rdy = 0, s_regs = 0, s_chain = 0, s_red = 0;
+    if (st_on) s_in = __builtin_amdgcn_s_memrealtime();
     // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
     float bb[ONE_NT_MAX];
 #pragma unroll
@@ -200,14 +219,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
             ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), zneed, scr + 240, c, true);
     }
-    if (a.ts && t == a.ts_step && lane == 0) {     // (stamps only, no barrier: this wave's inputs are there)
-        const unsigned long long r = __builtin_amdgcn_s_memrealtime();
-        atomicMax(a.ts + o * 4 + 3, r);
-        if (dg) {
-            atomicMax(dts + 1, r);
-            atomicMin(dts + 6, r);
-        }
-    }
+    if (st_on) s_rdy = __builtin_amdgcn_s_memrealtime();     // (this wave's inputs are there)
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
     __builtin_amdgcn_wave_barrier();
@@ -254,10 +266,9 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         f4 wv[LL];
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) wv[cc] = wt[(kb0 + max(min(cc, n - 1), 0)) * 64];
-        const bool dgt = dg && nt == 0 && lane == 0;
-        if (dgt) {
+        if (st_on && s_regs == 0) {
             __builtin_amdgcn_s_waitcnt(0xC07F);
-            atomicMax(dts + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+            s_regs = __builtin_amdgcn_s_memrealtime();
         }
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
@@ -267,12 +278,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             acc = (cc < LL - 1 || cc < n) ? t : acc;    // n >= LL - 1: only the last fragment can be discarded
         }
         if (lane < 16) red[wave * 16 + lane] = acc[0];     // row 0, column lane
-        if (dgt)    // (after the chain's result)
-            atomicMax(dts + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1 : 0));
+        if (st_on && s_chain == 0)    // (after the chain's result)
+            s_chain = __builtin_amdgcn_s_memrealtime() + (__builtin_amdgcn_readfirstlane(__float_as_int(acc[0])) == 1 ? 1 : 0);
         __syncthreads();
-        if (dgt && threadIdx.x == 0) dts[4] = __builtin_amdgcn_s_memrealtime();
-        if (a.ts && t == a.ts_step && threadIdx.x == 0)
-            atomicMax(a.ts + o * 4 + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (st_on && s_red == 0) s_red = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x < 16) {
             const int e = threadIdx.x, col = nt * 16 + e;
             float vv = red[e];
@@ -305,9 +314,28 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         }
         __syncthreads();
     }
-    if (a.ts && t == a.ts_step && threadIdx.x == 0)
-        atomicMax(a.ts + o * 4 + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    if (dg && threadIdx.x == 0) dts[5] = __builtin_amdgcn_s_memrealtime();
+    if (st_on) {
+        const unsigned long long s_pub = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* dts = a.ts + ONE_TS_DETAIL + o * ONE_TS_PER_OP;
+        if (lane == 0) {
+            atomicMax(a.ts + o * 4 + 3, s_rdy);
+            if (dg) {
+                dts[1 + wave] = s_rdy;
+                dts[1 + KSPLIT + wave] = s_regs;
+                dts[1 + 2 * KSPLIT + wave] = s_chain;
+            }
+        }
+        if (threadIdx.x == 0) {
+            atomicMin(a.ts + o * 4, s_in);
+            atomicMax(a.ts + o * 4 + 1, s_red);
+            atomicMax(a.ts + o * 4 + 2, s_pub);
+            if (dg) {
+                dts[0] = s_in;
+                dts[1 + 3 * KSPLIT] = s_red;
+                dts[2 + 3 * KSPLIT] = s_pub;
+            }
+        }
+    }
     // a uniform verdict for the whole workgroup
     if (!ok && lane == 0) *sflag = 1;
     __syncthreads();
@@ -396,15 +424,20 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
         ltab = reinterpret_cast<const uint16_t*>(wl);
     }
     __syncthreads();
+    int last_q = -(1 << 30);     // t * nops + o of the last operation this workgroup ran
     for (int t = 0; t < a.Hb * a.Wb; ++t) {
         const int v = t / a.Wb, h = t - v * a.Wb;
         const unsigned tag = (unsigned)t + 1u;
         for (int o = 0; o < a.nops; ++o) {
+            const int q = t * a.nops + o;
             if (o == a.rans_op) {
                 if (rank != a.rans_wg) continue;
+                if (a.gate > 0 && q - last_q >= a.gate && wave == 0) one_gate(a, o, tag, scr, c);
+                last_q = q;
                 bool ok = true;
-                const bool stamp = a.ts && t == a.ts_step && threadIdx.x == 0;
-                if (stamp) a.ts[o * 4] = __builtin_amdgcn_s_memrealtime();
+                const bool stamp = a.ts && t == a.ts_step;
+                unsigned long long r_in = 0, r_rdy = 0, r_coded = 0, r_pub = 0, c_rdy = 0, c_coded = 0;
+                if (stamp) r_in = __builtin_amdgcn_s_memrealtime();
                 if (wave == 0) {
                     // scale indexes | means of the context net (2 Mlat granules: ctx3's epilogue turned the scales into
                     // their indexes) into LDS
@@ -414,10 +447,9 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                         ok = wave_wait_gran(ctx.gran, g0, min(256, 2 * M - g0), tag, l_ksi + g0, c);
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
-                    if (stamp) a.ts[o * 4 + 1] = __builtin_amdgcn_s_memrealtime();
                     if (stamp) {
-                        a.ts[ONE_MAXOPS * 4] = __builtin_amdgcn_s_memrealtime();
-                        a.ts[ONE_MAXOPS * 4 + 2] = __builtin_amdgcn_s_memtime();    // (the shader clock: see below)
+                        r_rdy = __builtin_amdgcn_s_memrealtime();
+                        c_rdy = __builtin_amdgcn_s_memtime();    // (the shader clock)
                     }
                     if (ok) {
                         rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache,
@@ -425,12 +457,22 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
                         if (stamp) {
-                            a.ts[ONE_MAXOPS * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-                            a.ts[ONE_MAXOPS * 4 + 3] = __builtin_amdgcn_s_memtime();
+                            r_coded = __builtin_amdgcn_s_memrealtime();
+                            c_coded = __builtin_amdgcn_s_memtime();
                         }
                         const OneOp& yo = *(const OneOp*)((cop_p)a.ops + o);
                         for (int i = lane; i < yo.gw; i += 64) st_gran(yo.gran + i, i < M ? l_yq[i] : 0.f, tag);
-                        if (stamp) a.ts[o * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+                        if (stamp) r_pub = __builtin_amdgcn_s_memrealtime();
+                    }
+                    if (stamp && lane == 0) {
+                        a.ts[o * 4] = r_in;
+                        a.ts[o * 4 + 1] = r_coded;
+                        a.ts[o * 4 + 2] = r_pub;
+                        a.ts[o * 4 + 3] = r_rdy;
+                        a.ts[ONE_MAXOPS * 4] = r_rdy;
+                        a.ts[ONE_MAXOPS * 4 + 1] = r_coded;
+                        a.ts[ONE_MAXOPS * 4 + 2] = c_rdy;
+                        a.ts[ONE_MAXOPS * 4 + 3] = c_coded;
                     }
                     if (!ok && lane == 0) *sflag = 1;
                 }
@@ -444,9 +486,9 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
 #pragma unroll
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
-            if (a.ts && t == a.ts_step && threadIdx.x == 0)
-                atomicMin(a.ts + o * 4, (unsigned long long)__builtin_amdgcn_s_memrealtime());
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
+            if (a.gate > 0 && q - last_q >= a.gate) one_gate(a, o, tag, scr + wave * ONE_SCR, c);
+            last_q = q;
             if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c)) return;
         }
     }

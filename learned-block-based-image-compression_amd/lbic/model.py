@@ -288,10 +288,10 @@ class BlockBasedImgCompLossyNetv9:
 
     def one_phase_stamps(self):
         """The phases of the sampled raster step in the workgroup holding column tile 0 of each GEMM operation (the
-        same launch as one_stamps): per op [in, first wave's inputs there, last wave's inputs there, its A and weights
-        in registers, its chain done, partials reduced, published] in us relative to the first operation's first entry
-        (Nones for the rANS op)."""
-        words = 52 + 12 * 8
+        same launch as one_stamps): per op [in, first wave's inputs there, last wave's inputs there, last wave's A and
+        weights in registers, last chain done, partials reduced, published] in us relative to the first operation's
+        first entry (Nones for the rANS op), then the per-wave input times."""
+        per, words = 32, 52 + 12 * 32
         arr = (ctypes.c_ulonglong * words)()
         n = ctypes.c_int()
         _lib.check(_lib.lib().lbc_one_stamps(self._h, arr, words, ctypes.byref(n)))
@@ -302,8 +302,11 @@ class BlockBasedImgCompLossyNetv9:
         rel = lambda x: round((x - t0) / 100.0, 2) if x and x != 2 ** 64 - 1 else None
         out = []
         for o in range(12):
-            d = v[52 + 8 * o: 60 + 8 * o]
-            out.append([rel(d[k]) for k in (0, 6, 1, 2, 3, 4, 5)])
+            d = v[52 + per * o: 52 + per * (o + 1)]
+            rdy = [x for x in d[1:9] if x]
+            mx = lambda a: max(a) if a else 0
+            out.append([rel(d[0]), rel(min(rdy) if rdy else 0), rel(mx(rdy)), rel(mx(d[9:17])), rel(mx(d[17:25])),
+                        rel(d[25]), rel(d[26]), [rel(x) for x in d[1:9]]])
         return out
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:
