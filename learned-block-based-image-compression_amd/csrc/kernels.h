@@ -180,12 +180,9 @@ struct OneArgs {
     unsigned long long tmo;  // s_memrealtime ticks one wait may take
     int lazy_z;              // 1 (Wb >= 3): a d3 producer drains its zpad store of step t only before publishing step t + 1
     int rans_lds_tab;        // 1: the rANS workgroup copies the table image into its (weight-free) LDS
-    int gate;                // > 0: a workgroup whose previous operation is >= gate operations back first watches ONE
-                             // granule of the operation two before the one it waits for (one lane per wave), then polls
-                             // its inputs (the far waiters' full polls off the memory side)
     int ts_step;             // the sampled raster step of `ts`
-    unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step (kept in registers, written after
-                             // each op's publish): [0] first workgroup in, [1] last workgroup's partials reduced, [2]
+    unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step (kept in registers and LDS, written
+                             // after the last step): [0] first workgroup in, [1] last workgroup's partials reduced, [2]
                              // last one published, [3] the last wave's inputs all there; then [ONE_MAXOPS * 4] the
                              // rANS op's decode started (inputs in LDS), [+ 1] its symbols decoded, [+ 2], [+ 3]
                              // s_memtime (shader clock) at those two points; then [ONE_TS_DETAIL + ONE_TS_PER_OP o] the

@@ -630,8 +630,9 @@ template <bool SC1 = false, bool PERSIST = false, bool LOCAL = false>
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true,
                                                 const uint16_t* tab = nullptr, uint32_t* lc = nullptr,
                                                 const int32_t* lidx = nullptr, const float* lksi = nullptr,
-                                                float* lyq = nullptr) {
+                                                float* lyq = nullptr, unsigned long long* rts = nullptr) {
     RSTAMP(0);
+    unsigned long long rt1 = 0, rt2 = 0;     // (rts: prologue done, symbols done; written at the end)
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
     int img = row;
@@ -723,6 +724,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     __builtin_amdgcn_wave_barrier();
     if (!valid) return;
     RSTAMP(1);
+    if (rts) rt1 = __builtin_amdgcn_s_memrealtime();
     // every table's centre frequency <= 65534 (a table with a single-value pmf has 65535: then every step is tested).
     // Measured (round 4, profiles/r04_onecheck.txt): rANS operation 9.5-9.7 -> 9.2-9.4 us, decode alone -1.4 %.
     const bool one_check = __ballot(((uint32_t)t_lf >> 16) > 65534u) == 0ull;
@@ -863,6 +865,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         }
     }
     RSTAMP(2);
+    if (rts) rt2 = __builtin_amdgcn_s_memrealtime();
     bad |= p > nw;
     bad |= (p - p0 > RANS_WIN) ? 8 : 0;
 #pragma unroll
@@ -897,6 +900,10 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
             lc[3] = (uint32_t)p0;
             lc[4] = 1u;
         }
+    }
+    if (rts && lane == 0) {
+        rts[0] = rt1;
+        rts[1] = rt2;
     }
     RSTAMP(3);
 }

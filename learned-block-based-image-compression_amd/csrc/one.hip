@@ -106,22 +106,6 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     }
 }
 
-// The gate of a far waiter: until the operation two before `o` (in raster-step order) has published its first granule,
-// the inputs of `o` cannot be complete; watching that one granule (one lane per wave) keeps the 64-lane polls of
-// workgroups that wait far ahead of the chain off the memory side, and leaves them at least one operation of slack to
-// start polling before their inputs land.
-__device__ __forceinline__ void one_gate(const OneArgs& a, int o, unsigned tag, float* scr, const OneCtl& c) {
-    int so = o - 2;
-    unsigned st = tag;
-    if (so < 0) {
-        so += a.nops;
-        st -= 1u;
-    }
-    if (st == 0u) return;
-    const OneOp& s = *(const OneOp*)((cop_p)a.ops + so);
-    (void)wave_wait_gran(s.gran, 0, 1, st, scr, c, true);
-}
-
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     int x = my[0].x, y = my[0].y, z = my[0].z;
@@ -155,7 +139,7 @@ __device__ __forceinline__ int seg_of(const OneOp& op, int kb) {
 template <int LL>
 __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v,
                                          int h, unsigned tag, const f4* wl, float* red, float* scr_all, int* sflag,
-                                         const OneCtl& c) {
+                                         const OneCtl& c, unsigned long long* lst) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = op.K >> 4;
@@ -164,15 +148,9 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     bool ok = true;
     const OneOp& last = *(const OneOp*)((cop_p)a.ops + (a.nops - 1));    // d3: the reconstruction of every step
     const int t = (int)tag - 1;
-    // (stamps only, step ts_step) times kept in registers and written after the publish, so that no stamp store or
-    // atomic sits in the memory queue the op's own waits drain; dg: this workgroup holds column tile 0 of the op and
-    // also records every wave's phases
+    // (stamps only, step ts_step) times kept in registers, then in this workgroup's LDS stamp slot of the op (written to
+    // memory after the last step: no stamp store or atomic may sit in a memory queue that a wait drains)
     const bool st_on = a.ts && t == a.ts_step;
-    bool dg = false;
-    if (st_on) {
-#pragma unroll
-        for (int i = 0; i < ONE_NT_MAX; ++i) dg |= my[i].x == o && my[i].y == 0;
-    }
     unsigned long long s_in = 0, s_rdy = 0, s_regs = 0, s_chain = 0, s_red = 0;
     if (st_on) s_in = __builtin_amdgcn_s_memrealtime();
     // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
@@ -315,25 +293,19 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         __syncthreads();
     }
     if (st_on) {
-        const unsigned long long s_pub = __builtin_amdgcn_s_memrealtime();
-        unsigned long long* dts = a.ts + ONE_TS_DETAIL + o * ONE_TS_PER_OP;
+        int sl = 0;
+#pragma unroll
+        for (int i = ONE_NT_MAX - 1; i >= 0; --i) sl = my[i].x == o ? i : sl;
+        unsigned long long* d = lst + sl * ONE_TS_PER_OP;
         if (lane == 0) {
-            atomicMax(a.ts + o * 4 + 3, s_rdy);
-            if (dg) {
-                dts[1 + wave] = s_rdy;
-                dts[1 + KSPLIT + wave] = s_regs;
-                dts[1 + 2 * KSPLIT + wave] = s_chain;
-            }
+            d[1 + wave] = s_rdy;
+            d[1 + KSPLIT + wave] = s_regs;
+            d[1 + 2 * KSPLIT + wave] = s_chain;
         }
         if (threadIdx.x == 0) {
-            atomicMin(a.ts + o * 4, s_in);
-            atomicMax(a.ts + o * 4 + 1, s_red);
-            atomicMax(a.ts + o * 4 + 2, s_pub);
-            if (dg) {
-                dts[0] = s_in;
-                dts[1 + 3 * KSPLIT] = s_red;
-                dts[2 + 3 * KSPLIT] = s_pub;
-            }
+            d[0] = s_in;
+            d[1 + 3 * KSPLIT] = s_red;
+            d[2 + 3 * KSPLIT] = __builtin_amdgcn_s_memrealtime();
         }
     }
     // a uniform verdict for the whole workgroup
@@ -347,7 +319,8 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
 // LL = fragments per wave: L = (K / 16) / 8 k-blocks per slice, L + 1 when the slices differ in length (the extra
 // fragment's MFMAs are discarded), L when every slice has exactly L (nothing to discard: a shorter chain)
 __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v, int h,
-                             unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c) {
+                             unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c,
+                             unsigned long long* lst) {
     const int nkb = op.K >> 4;
     int key = (nkb / KSPLIT) * 2 + (nkb % KSPLIT == 0 ? 1 : 0);
 #ifndef LBIC_ONE_EXACT_ALL
@@ -355,9 +328,9 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 #endif
     switch (key) {
 #define LBIC_ONE(L_) \
-    case L_ * 2: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
+    case L_ * 2: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst);
 #define LBIC_ONE_EX(L_) \
-    case L_ * 2 + 1: return one_gemm<L_>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c);
+    case L_ * 2 + 1: return one_gemm<L_>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst);
         LBIC_ONE(0) LBIC_ONE(1) LBIC_ONE(2) LBIC_ONE(3) LBIC_ONE(4) LBIC_ONE(5) LBIC_ONE(6) LBIC_ONE(7) LBIC_ONE(8)
         LBIC_ONE(9) LBIC_ONE(10) LBIC_ONE(11)
 #ifdef LBIC_ONE_EXACT_ALL
@@ -374,10 +347,11 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 }  // namespace
 
 // dynamic LDS: [weight tiles wlds_f4 float4s][partials KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
-// [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words]
+// [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words][stamp slots ONE_NT_MAX x ONE_TS_PER_OP
+// u64]
 size_t one_lds_bytes(int wlds_f4) {
     return (size_t)wlds_f4 * 16 + (size_t)(KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
-           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4;
+           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8;
 }
 
 __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
@@ -390,6 +364,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     float* l_ksi = reinterpret_cast<float*>(rcache + ONE_RC_WORDS);
     float* l_yq = l_ksi + 512;
     int* sflag = reinterpret_cast<int*>(l_yq + 256);
+    unsigned long long* lst = reinterpret_cast<unsigned long long*>(sflag + 4);    // (8-byte aligned)
     const int rank = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -413,6 +388,8 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
         rcache[4] = 0u;    // no cached coder state yet
         *sflag = 0;
     }
+    if (a.ts)
+        for (int i = threadIdx.x; i < ONE_NT_MAX * ONE_TS_PER_OP; i += blockDim.x) lst[i] = 0ull;
     const RansArgs& R = *(const RansArgs*)((const __attribute__((address_space(4))) RansArgs*)a.rans);
     // the stream's workgroup holds no weights: its LDS takes a copy of the table image, so the rare symbols off the
     // centre intervals are searched in LDS instead of global memory (two dependent loads each)
@@ -424,16 +401,12 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
         ltab = reinterpret_cast<const uint16_t*>(wl);
     }
     __syncthreads();
-    int last_q = -(1 << 30);     // t * nops + o of the last operation this workgroup ran
     for (int t = 0; t < a.Hb * a.Wb; ++t) {
         const int v = t / a.Wb, h = t - v * a.Wb;
         const unsigned tag = (unsigned)t + 1u;
         for (int o = 0; o < a.nops; ++o) {
-            const int q = t * a.nops + o;
             if (o == a.rans_op) {
                 if (rank != a.rans_wg) continue;
-                if (a.gate > 0 && q - last_q >= a.gate && wave == 0) one_gate(a, o, tag, scr, c);
-                last_q = q;
                 bool ok = true;
                 const bool stamp = a.ts && t == a.ts_step;
                 unsigned long long r_in = 0, r_rdy = 0, r_coded = 0, r_pub = 0, c_rdy = 0, c_coded = 0;
@@ -453,7 +426,8 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                     }
                     if (ok) {
                         rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache,
-                                                           reinterpret_cast<const int32_t*>(l_ksi), l_ksi, l_yq);
+                                                           reinterpret_cast<const int32_t*>(l_ksi), l_ksi, l_yq,
+                                                           stamp ? lst + 8 : nullptr);
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
                         if (stamp) {
@@ -465,14 +439,12 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                         if (stamp) r_pub = __builtin_amdgcn_s_memrealtime();
                     }
                     if (stamp && lane == 0) {
-                        a.ts[o * 4] = r_in;
-                        a.ts[o * 4 + 1] = r_coded;
-                        a.ts[o * 4 + 2] = r_pub;
-                        a.ts[o * 4 + 3] = r_rdy;
-                        a.ts[ONE_MAXOPS * 4] = r_rdy;
-                        a.ts[ONE_MAXOPS * 4 + 1] = r_coded;
-                        a.ts[ONE_MAXOPS * 4 + 2] = c_rdy;
-                        a.ts[ONE_MAXOPS * 4 + 3] = c_coded;
+                        lst[0] = r_in;
+                        lst[1] = r_coded;
+                        lst[2] = r_pub;
+                        lst[3] = r_rdy;
+                        lst[4] = c_rdy;
+                        lst[5] = c_coded;
                     }
                     if (!ok && lane == 0) *sflag = 1;
                 }
@@ -487,9 +459,44 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
-            if (a.gate > 0 && q - last_q >= a.gate) one_gate(a, o, tag, scr + wave * ONE_SCR, c);
-            last_q = q;
-            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c)) return;
+            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst)) return;
+        }
+    }
+    // the stamps of step ts_step, from LDS to memory after the last step
+    if (a.ts) {
+        __syncthreads();
+        if (rank == a.rans_wg) {
+            if (threadIdx.x == 0) {
+                const int o = a.rans_op;
+                a.ts[o * 4] = lst[0];
+                a.ts[o * 4 + 1] = lst[1];
+                a.ts[o * 4 + 2] = lst[2];
+                a.ts[o * 4 + 3] = lst[3];
+                a.ts[ONE_MAXOPS * 4] = lst[3];
+                a.ts[ONE_MAXOPS * 4 + 1] = lst[1];
+                a.ts[ONE_MAXOPS * 4 + 2] = lst[4];
+                a.ts[ONE_MAXOPS * 4 + 3] = lst[5];
+                a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP] = lst[8];
+                a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP + 1] = lst[9];
+            }
+        } else if (threadIdx.x < ONE_NT_MAX) {
+            const int i = threadIdx.x;
+            const int4 ti = pick(my, i);
+            const int o = ti.x;
+            bool first = o >= 0;
+#pragma unroll
+            for (int j = 0; j < ONE_NT_MAX; ++j) first &= !(j < i && my[j].x == o);
+            if (first) {
+                const unsigned long long* d = lst + i * ONE_TS_PER_OP;
+                unsigned long long r = 0;
+                for (int w = 0; w < KSPLIT; ++w) r = d[1 + w] > r ? d[1 + w] : r;
+                atomicMin(a.ts + o * 4, d[0]);
+                atomicMax(a.ts + o * 4 + 1, d[1 + 3 * KSPLIT]);
+                atomicMax(a.ts + o * 4 + 2, d[2 + 3 * KSPLIT]);
+                atomicMax(a.ts + o * 4 + 3, r);
+                if (ti.y == 0)
+                    for (int k = 0; k < ONE_TS_PER_OP; ++k) a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP + k] = d[k];
+            }
         }
     }
 }

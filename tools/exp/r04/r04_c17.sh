@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4, GPU call 17: k_dec_one stamps in LDS, written to memory after the last step (the stamped step no longer
+# perturbed); rANS coder phases; gate removed.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_one_gpu.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/r04_c17_tests.log 2>&1 || { echo "tests failed"; tail -40 $O/r04_c17_tests.log; exit 3; }
+tail -1 $O/r04_c17_tests.log
+for v in a b; do
+  REPS=5 timeout -k 10 300 python3 -u tools/one_exp.py > $O/r04_c17_one_$v.log 2>&1 || { echo "one_exp $v failed"; tail -10 $O/r04_c17_one_$v.log; exit 4; }
+  echo "== $v"; grep '^{' $O/r04_c17_one_$v.log
+done
