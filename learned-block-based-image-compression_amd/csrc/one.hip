@@ -106,6 +106,40 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     }
 }
 
+// The same wait for a whole K slice of one granule source, loaded straight in the MFMA A layout: fragment cc, lane
+// 16 q + r holds k = 16 cc + 4 q + 0..3 (granules [g0 + 16 cc + 4 q, + 4) as two 16-byte sc1 loads; the 16 lanes of a
+// q load the same bytes, so rows 1-15 repeat row 0, and an MFMA row depends only on its own A row).  No scratch round
+// trip through LDS between the poll and the chain.  Fragments cc >= n are zero.
+template <int LL>
+__device__ __forceinline__ bool wave_wait_frag(const unsigned long long* gran, int g0, int n, unsigned tag, f4 (&av)[LL],
+                                               const OneCtl& c) {
+    const int lane = threadIdx.x & 63;
+    const unsigned base = (unsigned)(g0 + (lane >> 4) * 4) * 8u;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0;; ++it) {
+        bool ok = true;
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) {
+            uint4 p0 = uint4{0u, tag, 0u, tag}, p1 = p0;
+            if (cc < n) {
+                p0 = ld16_sc1(gran, base + cc * 128u);
+                p1 = ld16_sc1(gran, base + cc * 128u + 16u);
+            }
+            ok &= p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
+            av[cc] = f4{__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z)};
+        }
+        if (__ballot(!ok) == 0ull) return true;
+        if ((it & 15) == 15 &&
+            __hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
+            if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     int x = my[0].x, y = my[0].y, z = my[0].z;
@@ -169,11 +203,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     unsigned zneed = 0;
     // (uniform) the common shape: the whole of K is one granule segment of one source op from its column c0
     const bool gran1 = op.nseg == 1 && op.seg[0].kind == ONE_GRAN;
+    f4 av[LL];
     if (gran1) {
-        if (n > 0) {
-            const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
-            ok = wave_wait_gran(src.gran, op.seg[0].c0 + (kb0 << 4), n * 16, tag, scr, c);
-        }
+        const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
+        ok = wave_wait_frag<LL>(src.gran, op.seg[0].c0 + (kb0 << 4), n, tag, av, c);
     } else
     for (int cb = 0; cb < n && ok;) {
         const int s = seg_of(op, kb0 + cb);
@@ -201,18 +234,18 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
     __builtin_amdgcn_wave_barrier();
-    f4 av[LL];
     const bool row0 = (lane & 15) == 0;
     const int q4 = (lane >> 4) * 4;
     const long cell = ((long)(v + 2) * a.Wp + (h + 2));
-    if (gran1) {      // every fragment from the wave's scratch: no per-k-block segment lookup
+    if (gran1) {      // already in registers; the layer input x into the scratch for a GDN / IGDN epilogue
+        if (op.epi == EPI_GDN || op.epi == EPI_IGDN) {
 #pragma unroll
-        for (int cc = 0; cc < LL; ++cc) {
-            const int ci = max(min(cc, n - 1), 0);
-            f4 x = *reinterpret_cast<const f4*>(scr + ci * 16 + q4);
-            x = row0 ? x : f4{0.f, 0.f, 0.f, 0.f};
-            if (op.sq) x = x * x;
-            av[cc] = x;
+            for (int cc = 0; cc < LL; ++cc)
+                if (cc < n && row0) *reinterpret_cast<f4*>(scr + cc * 16 + q4) = av[cc];
+        }
+        if (op.sq) {
+#pragma unroll
+            for (int cc = 0; cc < LL; ++cc) av[cc] = av[cc] * av[cc];
         }
     } else
 #pragma unroll
