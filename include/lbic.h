@@ -153,7 +153,7 @@ int lbc_decode_path(const lbc_model *m, int *path, int *timeouts);
  * then [48] the rANS operation's decode started, [49] its symbols decoded, [50], [51] s_memtime (shader clock)
  * at those two points; then 32 per operation from the workgroup holding its column tile 0: [52 + 32 o] in, [+1 + w]
  * wave w's inputs there, [+9 + w] its A and weights in registers, [+17 + w] its chain done, [+25] partials reduced,
- * [+26] published (436 words; every stamp is written after the operation's publish). */
+ * [+26] published, [+27] thread 0's granule store issued (436 words; written after the last step). */
 int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 
 /* decompress() of n_teams batches at once (reference format; no reference counterpart for the batching: the

@@ -188,7 +188,9 @@ struct OneArgs {
                              // s_memtime (shader clock) at those two points; then [ONE_TS_DETAIL + ONE_TS_PER_OP o] the
                              // workgroup holding column tile 0 of op o: [0] in, [1 + w] wave w's inputs there, [9 + w]
                              // its A and weights in registers, [17 + w] its chain done, [25] partials reduced,
-                             // [26] published
+                             // [26] published (the tile loop's barrier passed), [27] thread 0's granule store issued;
+                             // for the rANS op: [0] coder prologue done, [1] symbols decoded, [2] speculation breaks,
+                             // [3] +-1 symbols, [4] searched symbols
 };
 constexpr int ONE_TS_DETAIL = ONE_MAXOPS * 4 + 4;
 constexpr int ONE_TS_PER_OP = 32;

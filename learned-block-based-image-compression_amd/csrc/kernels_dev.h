@@ -633,6 +633,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                                                 float* lyq = nullptr, unsigned long long* rts = nullptr) {
     RSTAMP(0);
     unsigned long long rt1 = 0, rt2 = 0;     // (rts: prologue done, symbols done; written at the end)
+    uint32_t n_brk = 0, n_pm1 = 0, n_srch = 0;   // (rts: speculation breaks, +-1 symbols, searched symbols)
     const bool valid = row_in < a.rows;
     const int row = valid ? row_in : a.rows - 1;
     int img = row;
@@ -807,7 +808,10 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                         xv = step(xv, l2, f2, bad);
                         xv = step(xv, l3, f3, bad);
                     }
-                    if (__builtin_amdgcn_readfirstlane(bad)) break;
+                    if (__builtin_amdgcn_readfirstlane(bad)) {
+                        if (rts) ++n_brk;
+                        break;
+                    }
                     x = uni64(xv);
                     ii += 4;
                 }
@@ -823,6 +827,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                 const uint32_t dm = cum - (im & 0xffffu), dp = cum - (ip & 0xffffu);
                 const bool hm = dm < (im >> 16), hp = dp < (ip >> 16);
                 if (hm || hp) {
+                    if (rts) ++n_pm1;
                     const uint32_t fr = hm ? im >> 16 : ip >> 16, d = hm ? dm : dp;
                     x = (unsigned long long)fr * (x >> 16) + d;
                     renorm();
@@ -832,6 +837,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                 }
             }
             // another symbol: the two-level search of rans_row on the table image in global memory
+            if (rts) ++n_srch;
             const int fb = rdlane_i(sfb[kb], ii), S = rdlane_i(sS[kb], ii);
             const int lm2 = rdlane_i(slm[kb], ii), ca = rdlane_i(sca[kb], ii);
             const uint32_t cv = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(img16) + ca + lane2);
@@ -904,6 +910,9 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
     if (rts && lane == 0) {
         rts[0] = rt1;
         rts[1] = rt2;
+        rts[2] = n_brk;
+        rts[3] = n_pm1;
+        rts[4] = n_srch;
     }
     RSTAMP(3);
 }

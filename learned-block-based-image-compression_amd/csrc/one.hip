@@ -106,40 +106,6 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     }
 }
 
-// The same wait for a whole K slice of one granule source, loaded straight in the MFMA A layout: fragment cc, lane
-// 16 q + r holds k = 16 cc + 4 q + 0..3 (granules [g0 + 16 cc + 4 q, + 4) as two 16-byte sc1 loads; the 16 lanes of a
-// q load the same bytes, so rows 1-15 repeat row 0, and an MFMA row depends only on its own A row).  No scratch round
-// trip through LDS between the poll and the chain.  Fragments cc >= n are zero.
-template <int LL>
-__device__ __forceinline__ bool wave_wait_frag(const unsigned long long* gran, int g0, int n, unsigned tag, f4 (&av)[LL],
-                                               const OneCtl& c) {
-    const int lane = threadIdx.x & 63;
-    const unsigned base = (unsigned)(g0 + (lane >> 4) * 4) * 8u;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0;; ++it) {
-        bool ok = true;
-#pragma unroll
-        for (int cc = 0; cc < LL; ++cc) {
-            uint4 p0 = uint4{0u, tag, 0u, tag}, p1 = p0;
-            if (cc < n) {
-                p0 = ld16_sc1(gran, base + cc * 128u);
-                p1 = ld16_sc1(gran, base + cc * 128u + 16u);
-            }
-            ok &= p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
-            av[cc] = f4{__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z)};
-        }
-        if (__ballot(!ok) == 0ull) return true;
-        if ((it & 15) == 15 &&
-            __hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
-            if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     int x = my[0].x, y = my[0].y, z = my[0].z;
@@ -173,7 +139,7 @@ __device__ __forceinline__ int seg_of(const OneOp& op, int kb) {
 template <int LL>
 __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v,
                                          int h, unsigned tag, const f4* wl, float* red, float* scr_all, int* sflag,
-                                         const OneCtl& c, unsigned long long* lst) {
+                                         const OneCtl& c, unsigned long long* lst, const float* ltab) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = op.K >> 4;
@@ -185,7 +151,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     // (stamps only, step ts_step) times kept in registers, then in this workgroup's LDS stamp slot of the op (written to
     // memory after the last step: no stamp store or atomic may sit in a memory queue that a wait drains)
     const bool st_on = a.ts && t == a.ts_step;
-    unsigned long long s_in = 0, s_rdy = 0, s_regs = 0, s_chain = 0, s_red = 0;
+    unsigned long long s_in = 0, s_rdy = 0, s_regs = 0, s_chain = 0, s_red = 0, s_st = 0;
     if (st_on) s_in = __builtin_amdgcn_s_memrealtime();
     // the epilogue operands of this op's tiles (bias, read-only), requested before anything waits
     float bb[ONE_NT_MAX];
@@ -203,10 +169,11 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     unsigned zneed = 0;
     // (uniform) the common shape: the whole of K is one granule segment of one source op from its column c0
     const bool gran1 = op.nseg == 1 && op.seg[0].kind == ONE_GRAN;
-    f4 av[LL];
     if (gran1) {
-        const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
-        ok = wave_wait_frag<LL>(src.gran, op.seg[0].c0 + (kb0 << 4), n, tag, av, c);
+        if (n > 0) {
+            const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
+            ok = wave_wait_gran(src.gran, op.seg[0].c0 + (kb0 << 4), n * 16, tag, scr, c);
+        }
     } else
     for (int cb = 0; cb < n && ok;) {
         const int s = seg_of(op, kb0 + cb);
@@ -234,18 +201,18 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     // A fragments (row 0 = lanes 0, 16, 32, 48: k = kb 16 + 4 (lane >> 4) + 0..3; the other rows are zero)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's scratch stores are done
     __builtin_amdgcn_wave_barrier();
+    f4 av[LL];
     const bool row0 = (lane & 15) == 0;
     const int q4 = (lane >> 4) * 4;
     const long cell = ((long)(v + 2) * a.Wp + (h + 2));
-    if (gran1) {      // already in registers; the layer input x into the scratch for a GDN / IGDN epilogue
-        if (op.epi == EPI_GDN || op.epi == EPI_IGDN) {
+    if (gran1) {      // every fragment from the wave's scratch: no per-k-block segment lookup
 #pragma unroll
-            for (int cc = 0; cc < LL; ++cc)
-                if (cc < n && row0) *reinterpret_cast<f4*>(scr + cc * 16 + q4) = av[cc];
-        }
-        if (op.sq) {
-#pragma unroll
-            for (int cc = 0; cc < LL; ++cc) av[cc] = av[cc] * av[cc];
+        for (int cc = 0; cc < LL; ++cc) {
+            const int ci = max(min(cc, n - 1), 0);
+            f4 x = *reinterpret_cast<const f4*>(scr + ci * 16 + q4);
+            x = row0 ? x : f4{0.f, 0.f, 0.f, 0.f};
+            if (op.sq) x = x * x;
+            av[cc] = x;
         }
     } else
 #pragma unroll
@@ -320,8 +287,9 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             }
             // the context net's scale columns go out as their scale indexes (build_indexes, the int in the float's
             // bits): the rANS workgroup decodes from them directly, the search done here by 16 lanes per tile
-            if (op.epi == EPI_CTXIDX && col < a.Mlat) out = __int_as_float(scale_index(out, a.table));
+            if (op.epi == EPI_CTXIDX && col < a.Mlat) out = __int_as_float(scale_index(out, ltab));
             if (col < gw) st_gran(op.gran + col, out, tag);
+            if (st_on && s_st == 0) s_st = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
     }
@@ -339,6 +307,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
             d[0] = s_in;
             d[1 + 3 * KSPLIT] = s_red;
             d[2 + 3 * KSPLIT] = __builtin_amdgcn_s_memrealtime();
+            d[3 + 3 * KSPLIT] = s_st;
         }
     }
     // a uniform verdict for the whole workgroup
@@ -353,7 +322,7 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
 // fragment's MFMAs are discarded), L when every slice has exactly L (nothing to discard: a shorter chain)
 __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v, int h,
                              unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c,
-                             unsigned long long* lst) {
+                             unsigned long long* lst, const float* ltab) {
     const int nkb = op.K >> 4;
     int key = (nkb / KSPLIT) * 2 + (nkb % KSPLIT == 0 ? 1 : 0);
 #ifndef LBIC_ONE_EXACT_ALL
@@ -361,9 +330,9 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 #endif
     switch (key) {
 #define LBIC_ONE(L_) \
-    case L_ * 2: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst);
+    case L_ * 2: return one_gemm<L_ + 1>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
 #define LBIC_ONE_EX(L_) \
-    case L_ * 2 + 1: return one_gemm<L_>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst);
+    case L_ * 2 + 1: return one_gemm<L_>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
         LBIC_ONE(0) LBIC_ONE(1) LBIC_ONE(2) LBIC_ONE(3) LBIC_ONE(4) LBIC_ONE(5) LBIC_ONE(6) LBIC_ONE(7) LBIC_ONE(8)
         LBIC_ONE(9) LBIC_ONE(10) LBIC_ONE(11)
 #ifdef LBIC_ONE_EXACT_ALL
@@ -381,10 +350,10 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 
 // dynamic LDS: [weight tiles wlds_f4 float4s][partials KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
 // [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words][stamp slots ONE_NT_MAX x ONE_TS_PER_OP
-// u64]
+// u64][scale table 64]
 size_t one_lds_bytes(int wlds_f4) {
     return (size_t)wlds_f4 * 16 + (size_t)(KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
-           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8;
+           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8 + 64 * 4;
 }
 
 __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
@@ -398,6 +367,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     float* l_yq = l_ksi + 512;
     int* sflag = reinterpret_cast<int*>(l_yq + 256);
     unsigned long long* lst = reinterpret_cast<unsigned long long*>(sflag + 4);    // (8-byte aligned)
+    float* ltab_s = reinterpret_cast<float*>(lst + ONE_NT_MAX * ONE_TS_PER_OP);   // the scale table (scale_index)
     const int rank = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -423,6 +393,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     }
     if (a.ts)
         for (int i = threadIdx.x; i < ONE_NT_MAX * ONE_TS_PER_OP; i += blockDim.x) lst[i] = 0ull;
+    if (threadIdx.x < 64) ltab_s[threadIdx.x] = a.table[threadIdx.x];
     const RansArgs& R = *(const RansArgs*)((const __attribute__((address_space(4))) RansArgs*)a.rans);
     // the stream's workgroup holds no weights: its LDS takes a copy of the table image, so the rare symbols off the
     // centre intervals are searched in LDS instead of global memory (two dependent loads each)
@@ -492,7 +463,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
-            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst)) return;
+            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab_s)) return;
         }
     }
     // the stamps of step ts_step, from LDS to memory after the last step
@@ -509,8 +480,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                 a.ts[ONE_MAXOPS * 4 + 1] = lst[1];
                 a.ts[ONE_MAXOPS * 4 + 2] = lst[4];
                 a.ts[ONE_MAXOPS * 4 + 3] = lst[5];
-                a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP] = lst[8];
-                a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP + 1] = lst[9];
+                for (int k = 0; k < 5; ++k) a.ts[ONE_TS_DETAIL + o * ONE_TS_PER_OP + k] = lst[8 + k];
             }
         } else if (threadIdx.x < ONE_NT_MAX) {
             const int i = threadIdx.x;

@@ -289,8 +289,10 @@ class BlockBasedImgCompLossyNetv9:
     def one_phase_stamps(self):
         """The phases of the sampled raster step in the workgroup holding column tile 0 of each GEMM operation (the
         same launch as one_stamps): per op [in, first wave's inputs there, last wave's inputs there, last wave's A and
-        weights in registers, last chain done, partials reduced, published] in us relative to the first operation's
-        first entry, then the per-wave input times; for the rANS op [coder prologue done, symbols decoded]."""
+        weights in registers, last chain done, partials reduced, thread 0's granule store issued, published (the tile
+        loop's closing barrier)] in us relative to the first operation's
+        first entry, then the per-wave input times; for the rANS op [coder prologue done, symbols decoded, speculation breaks, +-1 symbols,
+        searched symbols]."""
         per, words = 32, 52 + 12 * 32
         arr = (ctypes.c_ulonglong * words)()
         n = ctypes.c_int()
@@ -303,13 +305,13 @@ class BlockBasedImgCompLossyNetv9:
         out = []
         for o in range(12):
             d = v[52 + per * o: 52 + per * (o + 1)]
-            if o == 4:      # the rANS op: coder prologue done, symbols done
-                out.append([rel(d[0]), rel(d[1])])
+            if o == 4:      # the rANS op: coder prologue done, symbols done, speculation breaks, +-1, searched
+                out.append([rel(d[0]), rel(d[1]), d[2], d[3], d[4]])
                 continue
             rdy = [x for x in d[1:9] if x]
             mx = lambda a: max(a) if a else 0
             out.append([rel(d[0]), rel(min(rdy) if rdy else 0), rel(mx(rdy)), rel(mx(d[9:17])), rel(mx(d[17:25])),
-                        rel(d[25]), rel(d[26]), [rel(x) for x in d[1:9]]])
+                        rel(d[25]), rel(d[27]), rel(d[26]), [rel(x) for x in d[1:9]]])
         return out
 
     def rans_decode_gpu(self, streams: Sequence[bytes], indexes: torch.Tensor) -> torch.Tensor:

@@ -58,7 +58,7 @@ def main():
           flush=True)
     d = m.one_phase_stamps()
     print(json.dumps(dict(phases_us={OPS[o]: d[o] for o in range(len(d))},
-                          keys=["in", "first_ready", "last_ready", "regs", "chain", "reduced", "published", "ready_by_wave"])), flush=True)
+                          keys=["in", "first_ready", "last_ready", "regs", "chain", "reduced", "stored", "published", "ready_by_wave"])), flush=True)
 
 
 if __name__ == "__main__":
