@@ -630,7 +630,8 @@ template <bool SC1 = false, bool PERSIST = false, bool LOCAL = false>
 __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwin, int row_in, int lane, bool wt = true,
                                                 const uint16_t* tab = nullptr, uint32_t* lc = nullptr,
                                                 const int32_t* lidx = nullptr, const float* lksi = nullptr,
-                                                float* lyq = nullptr, unsigned long long* rts = nullptr) {
+                                                float* lyq = nullptr, unsigned long long* rts = nullptr,
+                                                uint32_t* llf = nullptr) {
     RSTAMP(0);
     unsigned long long rt1 = 0, rt2 = 0;     // (rts: prologue done, symbols done; written at the end)
     uint32_t n_brk = 0, n_pm1 = 0, n_srch = 0;   // (rts: speculation breaks, +-1 symbols, searched symbols)
@@ -710,6 +711,7 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
         }
         const int sel = ti[kb] << 2;
         const int lf = __builtin_amdgcn_ds_bpermute(sel, t_lf);
+        if (llf) llf[kb * 64 + lane] = (uint32_t)lf;     // (symbol-ordered centre intervals for the vector runs)
         lov[kb] = lf & 0xffff;
         frv[kb] = (int)((uint32_t)lf >> 16);
         ivm[kb] = __builtin_amdgcn_ds_bpermute(sel, t_lfm);
@@ -816,7 +818,38 @@ __device__ __forceinline__ void rans_row_sparse(const RansArgs& a, uint32_t* lwi
                     ii += 4;
                 }
             };
-            if (one_check) spec(std::true_type{});
+            // llf (k_dec_one) and one_check: the same runs with the state in a VGPR (every lane the same value) and the
+            // four intervals as broadcast LDS reads, a group ahead -- the state chain then runs on the vector ALU
+            // (v_mad_u64_u32) instead of a 16-instruction scalar sequence per symbol, and no v_readlane waits
+            if (llf && one_check) {
+                if (ii + 4 <= cnt_i) {
+                    unsigned long long xv = x;
+                    asm volatile("" : "+v"(xv));
+                    const uint32_t* lb = llf + kb * 64;
+                    uint32_t q0 = lb[ii], q1 = lb[ii + 1], q2 = lb[ii + 2], q3 = lb[ii + 3];
+                    while (true) {
+                        const int nx = min(ii + 4, 60);
+                        uint32_t n0 = lb[nx], n1 = lb[nx + 1], n2 = lb[nx + 2], n3 = lb[nx + 3];
+                        asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+                        uint32_t bad = 0;
+                        unsigned long long y = step_nr(xv, q0 & 0xffffu, q0 >> 16, bad);
+                        y = step_nr(y, q1 & 0xffffu, q1 >> 16, bad);
+                        y = step_nr(y, q2 & 0xffffu, q2 >> 16, bad);
+                        y = step_nr(y, q3 & 0xffffu, q3 >> 16, bad);
+                        bad |= ((uint32_t)(y >> 32) | ((uint32_t)y >> 31)) == 0u ? 1u : 0u;
+                        if (__ballot(bad != 0u) != 0ull) {
+                            if (rts) ++n_brk;
+                            break;
+                        }
+                        xv = y;
+                        ii += 4;
+                        if (ii + 4 > cnt_i) break;
+                        q0 = n0; q1 = n1; q2 = n2; q3 = n3;
+                    }
+                    x = uni64(((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xv >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xv));
+                }
+            } else if (one_check) spec(std::true_type{});
             else spec(std::false_type{});
             while (ii < cnt_i && fast(rdlane((uint32_t)lov[kb], ii), rdlane((uint32_t)frv[kb], ii))) ++ii;
             if (ii >= cnt_i) break;

@@ -361,10 +361,11 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 
 // dynamic LDS: [weight tiles wlds_f4 float4s][partials KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
 // [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words][stamp slots ONE_NT_MAX x ONE_TS_PER_OP
-// u64][scale table 64]
+// u64][scale table 64][rANS centre intervals 256]
 size_t one_lds_bytes(int wlds_f4) {
     return (size_t)wlds_f4 * 16 + (size_t)(KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
-           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8 + 64 * 4;
+           (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8 + 64 * 4 +
+           256 * 4;
 }
 
 __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     int* sflag = reinterpret_cast<int*>(l_yq + 256);
     unsigned long long* lst = reinterpret_cast<unsigned long long*>(sflag + 4);    // (8-byte aligned)
     float* ltab_s = reinterpret_cast<float*>(lst + ONE_NT_MAX * ONE_TS_PER_OP);   // the scale table (scale_index)
+    uint32_t* l_lf = reinterpret_cast<uint32_t*>(ltab_s + 64);                     // the rANS wave's centre intervals
     const int rank = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                     if (ok) {
                         rans_row_sparse<false, true, true>(R, lwin, 0, lane, false, ltab, rcache,
                                                            reinterpret_cast<const int32_t*>(l_ksi), l_ksi, l_yq,
-                                                           stamp ? lst + 8 : nullptr);
+                                                           stamp ? lst + 8 : nullptr, l_lf);
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         __builtin_amdgcn_wave_barrier();
                         if (stamp) {
