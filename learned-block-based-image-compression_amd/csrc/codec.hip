@@ -1401,7 +1401,6 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     if (!m->one_ok) return LBC_OK;
     OneArgs a = m->one_args;
     if (const char* t = getenv("LBIC_ONE_TMO")) a.tmo = std::max(1ull, strtoull(t, nullptr, 10));   // test hook
-    if (const char* p = getenv("LBIC_ONE_PACE")) a.pace = std::max(0, atoi(p));                       // A/B switch
     const char* st = getenv("LBIC_ONE_STAMPS");
     std::vector<unsigned long long> ts0(ONE_TS_WORDS, 0ull);
     if (st && atoi(st)) {

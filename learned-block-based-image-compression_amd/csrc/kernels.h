@@ -180,7 +180,6 @@ struct OneArgs {
     unsigned long long tmo;  // s_memrealtime ticks one wait may take
     int lazy_z;              // 1 (Wb >= 3): a d3 producer drains its zpad store of step t only before publishing step t + 1
     int rans_lds_tab;        // 1: the rANS workgroup copies the table image into its (weight-free) LDS
-    int pace;                // > 0 (A/B switch): far waiters sleep (distance - 2) x pace s_memrealtime ticks first
     int ts_step;             // the sampled raster step of `ts`
     unsigned long long* ts;  // optional [ONE_MAXOPS][4] s_memrealtime of step ts_step (kept in registers and LDS, written
                              // after the last step): [0] first workgroup in, [1] last workgroup's partials reduced, [2]

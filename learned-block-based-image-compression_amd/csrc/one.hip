@@ -106,17 +106,6 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
     }
 }
 
-// Pacing (A/B switch): a workgroup whose next operation q is d >= 3 operations after the one it last ran sleeps until
-// (d - 2) x pace 10-ns ticks after that one ended before it starts polling, so far waiters keep their 64-lane polls off
-// the memory side for most of their wait.
-__device__ __forceinline__ void one_pace(const OneArgs& a, int q, int last_q, unsigned long long last_t) {
-    const int d = q - last_q;
-    if (d >= 3) {
-        const unsigned long long until = last_t + (unsigned long long)(d - 2) * (unsigned)a.pace;
-        while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
-    }
-}
-
 // my[i] without dynamic indexing into a register array (which would put the array in scratch)
 __device__ __forceinline__ int4 pick(const int4 (&my)[ONE_NT_MAX], int i) {
     int x = my[0].x, y = my[0].y, z = my[0].z;
@@ -418,15 +407,12 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
         ltab = reinterpret_cast<const uint16_t*>(wl);
     }
     __syncthreads();
-    int last_q = -(1 << 30);             // (pacing) the last operation this workgroup ran: t * nops + o, its end
-    unsigned long long last_t = 0;
     for (int t = 0; t < a.Hb * a.Wb; ++t) {
         const int v = t / a.Wb, h = t - v * a.Wb;
         const unsigned tag = (unsigned)t + 1u;
         for (int o = 0; o < a.nops; ++o) {
             if (o == a.rans_op) {
                 if (rank != a.rans_wg) continue;
-                if (a.pace) one_pace(a, t * a.nops + o, last_q, last_t);
                 bool ok = true;
                 const bool stamp = a.ts && t == a.ts_step;
                 unsigned long long r_in = 0, r_rdy = 0, r_coded = 0, r_pub = 0, c_rdy = 0, c_coded = 0;
@@ -472,10 +458,6 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                 const bool good = *sflag == 0;
                 __syncthreads();
                 if (!good) return;
-                if (a.pace) {
-                    last_q = t * a.nops + o;
-                    last_t = __builtin_amdgcn_s_memrealtime();
-                }
                 continue;
             }
             bool mine = false;
@@ -483,12 +465,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
-            if (a.pace) one_pace(a, t * a.nops + o, last_q, last_t);
             if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab_s)) return;
-            if (a.pace) {
-                last_q = t * a.nops + o;
-                last_t = __builtin_amdgcn_s_memrealtime();
-            }
         }
     }
     // the stamps of step ts_step, from LDS to memory after the last step

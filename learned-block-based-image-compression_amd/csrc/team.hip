@@ -529,7 +529,7 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 template <bool DENSE, bool RING>
 __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host (team_lds_bytes):
-    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][control CTL_WORDS words]
+    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][control CTL_WORDS words][rANS centre intervals 256 words]
     // [GEMM partials ni_max x KSPLIT x 256 floats]
     // [dense rANS only: the table image, total16 16-bit entries]  [RING only: 8 rings x ring_q x 1 KB]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
@@ -537,7 +537,8 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
     uint32_t* rcache = team_lds + RANS_WIN;                              // rans_row_sparse<.., true>'s state cache
     uint32_t* ctl = team_lds + RANS_WIN + RC_WORDS;
     int& sflag = *reinterpret_cast<int*>(ctl + 18);
-    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + CTL_WORDS);
+    uint32_t* llf = team_lds + RANS_WIN + RC_WORDS + CTL_WORDS;          // rans_row_sparse's vector runs
+    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + CTL_WORDS + 256);
     f4* ring = reinterpret_cast<f4*>(red + ta.ni_max * KSPLIT * 256);
     if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
     if (RING && threadIdx.x < CTL_WORDS) ctl[threadIdx.x] = 0u;
@@ -617,11 +618,13 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
                     if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
                         if (!DENSE && rank < R.rows && rank + S >= R.rows) {
                             // one image per workgroup, the same one at every step: the coder state stays in LDS
-                            rans_row_sparse<true, true>(R, lwin, rank, lane, wt, nullptr, rcache);
+                            rans_row_sparse<true, true>(R, lwin, rank, lane, wt, nullptr, rcache, nullptr, nullptr,
+                                                        nullptr, nullptr, llf);
                         } else {
                             for (int r = rank; r < R.rows; r += S) {
                                 if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
-                                else rans_row_sparse<true>(R, lwin, r, lane, wt);
+                                else rans_row_sparse<true>(R, lwin, r, lane, wt, nullptr, nullptr, nullptr, nullptr,
+                                                           nullptr, nullptr, llf);
                             }
                         }
                         if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
@@ -660,7 +663,7 @@ int team_blocks_per_cu(int dense, int ring, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + RC_WORDS + CTL_WORDS) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 +
+    return (size_t)(RANS_WIN + RC_WORDS + CTL_WORDS + 256) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 +
            (size_t)(a.dense ? 1 : 0) * a.tab16 * 2 + (size_t)a.ring_q * KSPLIT * 1024;
 }
 
