@@ -169,6 +169,23 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     unsigned zneed = 0;
     // (uniform) the common shape: the whole of K is one granule segment of one source op from its column c0
     const bool gran1 = op.nseg == 1 && op.seg[0].kind == ONE_GRAN;
+    // otherwise: each fragment's source resolved before the waits (the per-k-block segment lookup is a chain of scalar
+    // loads): bit cc of zmask (uniform) = a zpad tap at byte offset zo[cc], else the wave's scratch
+    const int q4 = (lane >> 4) * 4;
+    const long cell = ((long)(v + 2) * a.Wp + (h + 2));
+    unsigned zmask = 0;
+    unsigned zo[LL];
+    if (!gran1) {
+#pragma unroll
+        for (int cc = 0; cc < LL; ++cc) {
+            const int ci = max(min(cc, n - 1), 0);      // (an empty slice, n = 0, loads k-block kb0 and adds nothing)
+            const int kb = kb0 + ci;
+            const OneSeg& sg = op.seg[seg_of(op, kb)];
+            const bool z = sg.kind == ONE_ZTAP && !(sg.dy == 0 && sg.dx == -1 && h >= 1);
+            zmask |= z ? 1u << cc : 0u;
+            zo[cc] = (unsigned)((cell + (long)sg.dy * a.Wp + sg.dx) * a.Cx + (kb << 4) - sg.k0 + q4) * 4u;
+        }
+    }
     if (gran1) {
         if (n > 0) {
             const OneOp& src = *(const OneOp*)((cop_p)a.ops + op.seg[0].src);
@@ -203,8 +220,6 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     __builtin_amdgcn_wave_barrier();
     f4 av[LL];
     const bool row0 = (lane & 15) == 0;
-    const int q4 = (lane >> 4) * 4;
-    const long cell = ((long)(v + 2) * a.Wp + (h + 2));
     if (gran1) {      // every fragment from the wave's scratch: no per-k-block segment lookup
 #pragma unroll
         for (int cc = 0; cc < LL; ++cc) {
@@ -217,14 +232,10 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
     } else
 #pragma unroll
     for (int cc = 0; cc < LL; ++cc) {
-        const int ci = max(min(cc, n - 1), 0);      // (an empty slice, n = 0, loads k-block kb0 and adds nothing)
-        const int kb = kb0 + ci;
-        const int s = seg_of(op, kb);
-        const OneSeg& sg = op.seg[s];
+        const int ci = max(min(cc, n - 1), 0);
         f4 x = f4{0.f, 0.f, 0.f, 0.f};
-        if (sg.kind == ONE_ZTAP && !(sg.dy == 0 && sg.dx == -1 && h >= 1)) {
-            const unsigned off = (unsigned)((cell + (long)sg.dy * a.Wp + sg.dx) * a.Cx + (kb << 4) - sg.k0 + q4) * 4u;
-            const uint4 u = ld16_sc1(a.zpad, off);
+        if ((zmask >> cc) & 1u) {
+            const uint4 u = ld16_sc1(a.zpad, zo[cc]);
             x = row0 ? __builtin_bit_cast(f4, u) : x;
         } else {
             const f4 u = *reinterpret_cast<const f4*>(scr + ci * 16 + q4);

@@ -16,3 +16,10 @@ for v in main prev main prev; do
   timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --cpu-budget 0 --side-steps 0 --per-image 0 > $O/r04_c22_bench_$v.log 2>&1 || { echo "bench $v failed"; tail -5 $O/r04_c22_bench_$v.log; exit 6; }
   grep '^{' $O/r04_c22_bench_$v.log | python3 -c "import json,sys; j=json.loads(sys.stdin.read()); print('bench', sys.argv[1], j['value'], j['ms_per_step'], j['phases_ms_per_step'], j['kernels']['k_gemm']['avg_launch_us'], j['kernels']['k_dec_team']['launch_ms_per_batch'])" $v
 done
+# k_dec_one: the non-gran1 operations' fragment sources resolved before the waits (liblbic_zo.so) against main
+for v in main zo main zo; do
+  unset LBIC_LIB_VARIANT
+  if [ $v = zo ]; then export LBIC_LIB_VARIANT=zo; fi
+  REPS=5 timeout -k 10 300 python3 -u tools/one_exp.py > $O/r04_c22_one_$v.log 2>&1 || { echo "one_exp $v failed"; tail -10 $O/r04_c22_one_$v.log; exit 7; }
+  echo "== $v"; grep '"decoder": "one"' $O/r04_c22_one_$v.log
+done
