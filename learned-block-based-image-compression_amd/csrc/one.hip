@@ -94,14 +94,13 @@ __device__ __forceinline__ bool wave_wait_gran(const unsigned long long* gran, i
             }
             return true;
         }
-        // the failure word and the clock only every 16th poll: a poll is one memory round trip, and s_memrealtime is a
-        // scalar-memory read whose wait would lengthen every poll period
-        if ((it & 15) == 15) {
-            if (__hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
-                if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return false;
-            }
+        // the failure word only every 16th poll: a poll is one memory round trip, not two
+        if ((it & 15) == 15 &&
+            __hip_atomic_load((gptr<unsigned>)c.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > c.tmo) {
+            if (lane == 0) __hip_atomic_store((gptr<unsigned>)c.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
         }
         __builtin_amdgcn_s_sleep(1);
     }
