@@ -645,7 +645,7 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = world * n * H * W / (dt / args.steps) / 1e6
 
-    roof, kernels = roofline(kstats, dt, team_acc if args.team else None, enc_acc if args.team else None)
+    roof, kernels = roofline(kstats, dt, team_acc if args.team else None, enc_acc if args.team else None, args.steps)
     mac_enc, mac_dec = arch.live_macs_per_block()
     step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
     cpu = None
@@ -716,61 +716,64 @@ def gather_records(rec, ok, dist):
     return torch.cat(allrec), bool(flag.item() == 1.0)
 
 
-def roofline(kstats, dt, team=None, enc=None):
-    """Dominant kernel family (its time share of the timed region) against its roofline.  Graph-launched kernels:
-    the in-kernel timing stamps of the sampled launches executed in the timed region (lbc_profile_*):
-    `avg_launch_us` is the launch-to-launch period in the stream chain (end of the previous launch -> end of this
-    one: the launch's span plus the boundary in front of it, which is what a dispatch-to-completion trace measures),
-    `avg_span_us` the workgroups' own span; share = period x true launch count.  The team decoder (`team`, one
-    persistent launch per group of batches): HIP events around each launch, algorithmic bytes / FLOPs per launch from
-    the library (lbc_team_stats).  The encoder under the team schedule (`enc`, no sampling): HIP events around each
-    encoder graph divided by the graph's launches (k_gemm and its few small-M k_gemm_s ramp launches), algorithmic
-    work of all launches (lbc_kernel_stat.total_flops / total_bytes)."""
+def roofline(kstats, dt, team=None, enc=None, steps=0):
+    """Dominant kernel family against its roofline.  Dominance = wall occupancy in the timed region, i.e. the time
+    during which the family has a launch running, overlap with OTHER families allowed but never counted twice within
+    one family: for the team decoder the summed durations of its launches (one at a time, HIP events around each), for
+    the encoder's GEMM family the summed wall time of the encoder graphs (HIP events around each graph: its forked
+    branches run two of its launches at once, so the launches' summed durations exceed the graph's wall time and are
+    not its occupancy).  Graph-launched kernels: per-launch durations from the in-kernel timing stamps of the sampled
+    launches executed in the timed region (lbc_profile_*; earliest workgroup start -> latest end, what a dispatch trace
+    such as rocprofv3 --kernel-trace reports); the encoder family is also reported as an aggregate (its algorithmic
+    FLOPs over the encoder graphs' wall time).  The team decoder: algorithmic bytes / FLOPs per launch from the library
+    (lbc_team_stats)."""
     kernels, fam = {}, {}
     if enc is not None and kstats:
-        # the encoder graph forks every wavefront step into two branches that run concurrently, so graph time / launches
-        # (`wall_us_per_launch`) is not a launch's duration.  A launch's duration (what a dispatch trace such as rocprofv3
-        # --kernel-trace reports) comes from the in-kernel stamps of the sampled k_gemm launches: earliest workgroup
-        # start to latest workgroup end on the 100 MHz constant clock (lbc_profile_begin(sample_every))
-        n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
-        sg = kstats.get("k_gemm", {})
+        egm = "k_gemm_t" if "k_gemm_t" in kstats else "k_gemm"       # lbc_profile names the family by its kernel
+        n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
+        sg = kstats.get(egm, {})
         if n_all and enc["ms"] > 0:
             wall = enc["ms"] / n_all
-            tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
-            tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in ("k_gemm", "k_gemm_s"))
+            tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
+            tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
+            agg = dict(encoder_wall_s=round(enc["ms"] / 1e3, 4), encoder_graphs=enc["passes"],
+                       tflop=round(tf / 1e12, 4), achieved_tflops=round(tf / (enc["ms"] / 1e3) / 1e12, 3),
+                       frac=round(tf / (enc["ms"] / 1e3) / (PEAK_FP32_TFLOPS * 1e12), 5),
+                       note=f"every launch of the encoder graphs ({egm} + the k_gemm_s ramp steps): algorithmic FLOPs / "
+                            "the graphs' wall time")
             if sg.get("launches"):
                 per = sg["total_ms"] / sg["launches"]
                 n_k = int(sg["total_launches"])
-                kernels["k_gemm"] = dict(launches_sampled=int(sg["launches"]), launches_total=n_k,
-                                         avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
-                                         wall_us_per_launch=round(wall * 1e3, 3),
-                                         est_share_of_step=round(per * n_k / 1e3 / dt, 4),
-                                         timing="in-kernel stamps of the sampled k_gemm launches (earliest workgroup "
-                                                "start -> latest end; the forked branches overlap, so the summed "
-                                                f"durations exceed the encoder's wall time, {enc['ms'] / 1e3:.3f} s "
-                                                f"over {enc['passes']} encoder graphs)")
-                fam["k_gemm"] = (sg["flops"] / sg["launches"], sg["bytes"] / sg["launches"])
+                kernels[egm] = dict(launches_sampled=int(sg["launches"]), launches_total=n_k,
+                                    avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
+                                    wall_us_per_launch=round(wall * 1e3, 3),
+                                    wall_occupancy_s=round(enc["ms"] / 1e3, 4),
+                                    summed_launch_s=round(per * n_k / 1e3, 4), aggregate=agg,
+                                    timing=f"in-kernel stamps of the sampled {egm} launches (earliest workgroup start -> "
+                                           "latest end); occupancy = HIP events around the encoder graphs "
+                                           f"({enc['ms'] / 1e3:.3f} s over {enc['passes']} graphs)")
+                fam[egm] = (sg["flops"] / sg["launches"], sg["bytes"] / sg["launches"])
             else:
-                kernels["k_gemm"] = dict(launches_sampled=0, launches_total=int(n_all), avg_span_us=round(wall * 1e3, 3),
-                                         avg_launch_us=round(wall * 1e3, 3), wall_us_per_launch=round(wall * 1e3, 3),
-                                         est_share_of_step=round(enc["ms"] / 1e3 / dt, 4),
-                                         timing=f"HIP events around {enc['passes']} encoder graphs / their launches "
-                                                "(k_gemm + k_gemm_s ramp steps; the forked branches overlap, so this "
-                                                "understates a launch's own duration)")
-                fam["k_gemm"] = (tf / n_all, tb / n_all)
+                kernels[egm] = dict(launches_sampled=0, launches_total=int(n_all), avg_span_us=round(wall * 1e3, 3),
+                                    avg_launch_us=round(wall * 1e3, 3), wall_us_per_launch=round(wall * 1e3, 3),
+                                    wall_occupancy_s=round(enc["ms"] / 1e3, 4), aggregate=agg,
+                                    timing=f"HIP events around {enc['passes']} encoder graphs / their launches "
+                                           f"({egm} + k_gemm_s ramp steps; the forked branches overlap, so this "
+                                           "understates a launch's own duration)")
+                fam[egm] = (tf / n_all, tb / n_all)
         kstats = {}
     for name, s in (kstats or {}).items():
         span = s["total_ms"] / max(s["launches"], 1)
         per = s["total_ms_chain"] / s["launches_chain"] if s["launches_chain"] else span
         kernels[name] = dict(launches_sampled=int(s["launches"]), launches_total=int(s["total_launches"]),
                              avg_span_us=round(span * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
-                             est_share_of_step=round(per * s["total_launches"] / 1e3 / dt, 4))
+                             wall_occupancy_s=round(per * s["total_launches"] / 1e3, 4))
         fam[name] = (s["flops"] / max(s["launches"], 1), s["bytes"] / max(s["launches"], 1))
     if team and team["launches"]:
         per = team["ms"] / team["launches"]
         kernels["k_dec_team"] = dict(launches_sampled=team["launches"], launches_total=team["launches"],
                                      avg_span_us=round(per * 1e3, 3), avg_launch_us=round(per * 1e3, 3),
-                                     est_share_of_step=round(team["ms"] / 1e3 / dt, 4),
+                                     wall_occupancy_s=round(team["ms"] / 1e3, 4),
                                      plain_handoffs=team["plain"],
                                      barrier_timeout_fallbacks=team["timeouts"],
                                      batches_per_launch=round(team["steps"] / team["launches"] / team["hw"], 3),
@@ -780,9 +783,7 @@ def roofline(kstats, dt, team=None, enc=None):
         fam["k_dec_team"] = (team["flops"] / team["launches"], team["bytes"] / team["launches"])
     if not kernels:
         return None, {}
-    # dominant = the most summed launch duration in the timed region (a dispatch trace's "total duration"); with the
-    # encoder's forked branches and the team decoder running concurrently the summed durations exceed the region
-    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_total"])
+    dom = max(kernels, key=lambda k: kernels[k]["wall_occupancy_s"])
     if not fam[dom][1]:
         return None, kernels
     ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
@@ -793,35 +794,44 @@ def roofline(kstats, dt, team=None, enc=None):
         if fl_ > 0 and by_ and fl_ / by_ >= ridge:
             return fl_ / s_ / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
         return by_ / s_ / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+    traffic_db = {}
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/pmc_round.sh)
+        with open(tfile) as fh:
+            traffic_db = json.load(fh)
+
+    def traffic_of(name):
+        pm = traffic_db.get(name, {})
+        if name == "k_dec_team" and team and "hbm_bytes_per_team_step" in pm:
+            return round(pm["hbm_bytes_per_team_step"] * team["steps"] / team["launches"]), pm.get("source")
+        if "hbm_bytes_per_dispatch" in pm:
+            return round(pm["hbm_bytes_per_dispatch"]), pm.get("source")
+        return None, None
     per_kernel = {}
     for name in kernels:
         if name in fam and fam[name][1]:
             a_, p_, u_, b_ = bound_of(name)
+            tr_, src_ = traffic_of(name)
             per_kernel[name] = dict(bound=b_, achieved=round(a_, 4), peak=p_, unit=u_, frac=round(a_ / p_, 5),
                                     avg_launch_us=kernels[name]["avg_launch_us"],
-                                    summed_duration_s=round(kernels[name]["avg_launch_us"] *
-                                                            kernels[name]["launches_total"] * 1e-6, 4))
+                                    wall_occupancy_s=kernels[name]["wall_occupancy_s"],
+                                    algorithmic_per_launch=dict(flops=round(fam[name][0]), bytes=round(fam[name][1])),
+                                    traffic=tr_, traffic_source=src_)
+            if "aggregate" in kernels[name]:
+                per_kernel[name]["aggregate"] = kernels[name]["aggregate"]
     fl, by = fam[dom]
     ai = fl / by if by else float("inf")
     ach, peak, unit, bound = bound_of(dom)
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile):       # rocprofv3 PMC passes (tools/gpu_profile.sh, tools/team_pmc.sh)
-        with open(tfile) as fh:
-            pm = json.load(fh)
-        f_ = re.sub(r"<.*>$", "", dom)
-        if f_ == "k_dec_team" and team and "hbm_bytes_per_team_step" in pm.get(f_, {}):
-            traffic = round(pm[f_]["hbm_bytes_per_team_step"] * team["steps"] / team["launches"])
-        elif f_ in pm and "hbm_bytes_per_dispatch" in pm[f_]:
-            traffic = round(pm[f_]["hbm_bytes_per_dispatch"])
+    traffic, tsrc = traffic_of(dom)
     roof = dict(kernel=dom, bound=bound, achieved=round(ach, 4), peak=peak, unit=unit, frac=round(ach / peak, 5),
-                traffic=traffic, avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],
+                traffic=traffic, traffic_source=tsrc,
+                avg_launch_us=kernels[dom]["avg_launch_us"], avg_span_us=kernels[dom]["avg_span_us"],
                 algorithmic_per_launch=dict(flops=round(fl), bytes=round(by)), arithmetic_intensity=round(ai, 2),
-                frac_of_span=round((fl / (kernels[dom]["avg_span_us"] * 1e-6) / 1e12 / peak) if bound == "mfma" else
-                                   (by / (kernels[dom]["avg_span_us"] * 1e-6) / 1e9 / peak), 5),
+                wall_occupancy_s=kernels[dom]["wall_occupancy_s"],
+                wall_occupancy_ms_per_step=round(kernels[dom]["wall_occupancy_s"] * 1e3 / steps, 3) if steps else None,
                 per_kernel=per_kernel,
-                dominant_rule="largest summed launch duration in the timed region (avg launch duration x launches); "
-                              "concurrent kernels' summed durations may exceed the region")
+                dominant_rule="largest wall occupancy in the timed region: the time the family has a launch running "
+                              "(team decoder: summed launch durations; encoder GEMMs: the encoder graphs' wall time)")
     return roof, kernels
 
 

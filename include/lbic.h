@@ -177,12 +177,10 @@ int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, in
  * outputs; times teams x Hb x Wb) and whether it ran with plain hand-off stores (1) or write-through ones (0). */
 int lbc_team_stats(const lbc_model *m, double *launch_ms, double *bytes, double *flops, int *plain);
 /* how the last lbc_decode_team call led by m decoded: 0 lbc_decode per batch (fallback), 1 one team launch with the
- * sparse rANS variant, 2 one team launch with the dense variant (tables in LDS). */
+ * sparse rANS variant, 2 one team launch with the dense variant (tables in LDS); one batch of one image goes to
+ * lbc_decode: 3 its single-image decoder (k_dec_one), 4 its row graphs (lbc_team_stats then reports that decode's
+ * duration, no algorithmic work and plain = -1). */
 int lbc_team_mode(const lbc_model *m, int *mode);
-/* weight-ring slots per K slice of the last lbc_decode_team launch led by m: > 0 its GEMM weights were streamed into
- * LDS rings by loader waves (the default where the LDS allows: the sparse rANS variant, one workgroup per CU), 0 the
- * computing waves loaded them from global memory.  Results are identical either way. */
-int lbc_team_ring(const lbc_model *m, int *slots);
 /* counters of the lbc_decode_team calls led by m: launches rerun with write-through hand-offs after the placement
  * census found a team spread over XCDs; and launches in which a workgroup timed out at a team barrier (the grid was
  * not co-resident in time, e.g. CUs held by another process) and whose batches were then decoded by lbc_decode one

@@ -189,8 +189,6 @@ struct lbc_model {
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
     int team_wpc = 1;           // LBC_OPT_TEAM_WG_PER_CU
     int team_size = 0;          // LBC_OPT_TEAM_SIZE (0: CUs / 8)
-    int team_ll_max = 0;        // the recorded team program: most weight fragments of one item's K slice (fast path)
-    int team_ring_last = 0;     // ring slots per K slice of the last team launch (0: no weight ring)
     Work lane[kLanes];
     hipStream_t lstream[kLanes] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t lev[kLanes + 1] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -223,8 +221,10 @@ struct lbc_model {
     std::vector<unsigned long long> team_ts_host;
     int team_fallbacks = 0, team_plain_last = -1;   // launches rerun write-through; mode of the last launch
     int team_timeouts = 0;    // team launches that timed out at a barrier and were decoded through lbc_decode instead
-    int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch, 1 team + sparse rANS, 2 team + dense,
-                              // 3 one image through lbc_decode's single-image decoder (k_dec_one)
+    bool no_one = false;      // lbc_decode skips k_dec_one (set by team_fallback after a residency timeout)
+    int team_mode_last = 0;   // the last lbc_decode_team call: 0 lbc_decode per batch (a fallback), 1 team + sparse rANS,
+                              // 2 team + dense, one batch of one image through lbc_decode: 3 its single-image decoder
+                              // (k_dec_one), 4 its row graphs
     double team_step_bytes = 0, team_step_flops = 0;  // algorithmic work of one team's raster step (inner column)
     double team_launch_bytes = 0, team_launch_flops = 0;
     // single-image decoder (k_dec_one, one.hip; lbc_decode of one image): the step's operations, the weight-tile
@@ -595,12 +595,25 @@ int rans_sparse_choice(const size_t* lens, int n, double symbols) {
     return symbols > 0 && 8.0 * bytes / symbols < thr ? 1 : 0;
 }
 
-int check_status(lbc_model* m, size_t n, hipStream_t s) {
-    std::vector<int> status(n);
+// full: the decode consumed every block of every stream, so each rANS stream must end where its encoder began: state
+// RANS64_L = 2^31 (Rans64EncInit; the decoder retraces the encoder's states in reverse) with every word read.  A
+// truncated stream overruns (status); a corrupted one ends in another state with near certainty -- both raise.
+int check_status(lbc_model* m, size_t n, hipStream_t s, bool full) {
+    std::vector<int> status(n), ptr(full ? n : 0), cnt(full ? n : 0);
+    std::vector<unsigned long long> x(full ? n : 0);
     HIPCHK(hipMemcpyAsync(status.data(), m->st_status.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (full) {
+        HIPCHK(hipMemcpyAsync(x.data(), m->st_x.p, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ptr.data(), m->st_ptr.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(cnt.data(), m->word_count.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
-    for (size_t i = 0; i < n; ++i)
+    for (size_t i = 0; i < n; ++i) {
         if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream (stream " + std::to_string(i) + ")");
+        if (full && (x[i] != (1ull << 31) || ptr[i] != cnt[i]))
+            return set_error(LBC_E_STREAM, "corrupt bitstream (stream " + std::to_string(i) +
+                                               ": the decode does not end in the encoder's initial state)");
+    }
     return LBC_OK;
 }
 
@@ -1247,7 +1260,7 @@ int lbc_rans_decode_gpu(lbc_model* m, const uint8_t* const* streams, const size_
         rc = launch_rans_decode(r, s);
     }
     if (rc) return rc;
-    return check_status(m, (size_t)n_streams, s);
+    return check_status(m, (size_t)n_streams, s, false);
 }
 
 // ---------------------------------------------------------------------------------------------- single image
@@ -1394,7 +1407,9 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
 static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStream_t s, int* used) {
     *used = 0;
     const char* e = getenv("LBIC_ONE");
-    if ((e && atoi(e) == 0) || !rans_sparse_choice(lens, 1, (double)Hb * Wb * m->M)) return LBC_OK;
+    // (no_one: a team fallback after a residency timeout -- the chip's CUs are held elsewhere, and k_dec_one needs
+    // every one of them co-resident, so it would likely time out again: go to the row graphs directly)
+    if ((e && atoi(e) == 0) || m->no_one || !rans_sparse_choice(lens, 1, (double)Hb * Wb * m->M)) return LBC_OK;
     int cus = 0, rc;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->cfg.device));
     if ((rc = one_prepare(m, Hb, Wb, cus))) return rc;
@@ -1418,7 +1433,9 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     unsigned fail = 0;
     HIPCHK(hipMemcpyAsync(&fail, m->one_fail.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (fail) {
+    if (fail > 1)   // k_dec_one writes 1 (a wait timed out) and nothing else: any other word is a protocol error
+        return set_error(LBC_E_STATE, "single-image decode: unexpected failure word " + std::to_string(fail));
+    if (fail == 1) {
         m->one_timeouts += 1;
         static std::atomic<bool> noted{false};
         if (!noted.exchange(true))
@@ -1454,7 +1471,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
             if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
             HIPCHK(hipEventRecord(m->ev[3], s));
             m->dec_timed = true;
-            return check_status(m, (size_t)n_img, s);
+            return check_status(m, (size_t)n_img, s, true);
         }
         if (used == -1) {   // a timed-out launch advanced the coder state: start again
             if ((rc = upload_streams(m, subs, s))) return rc;
@@ -1569,7 +1586,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[3], s));
     m->dec_timed = true;
-    return check_status(m, (size_t)n_img, s);
+    return check_status(m, (size_t)n_img, s, true);
 }
 
 // ---------------------------------------------------------------------------------------------- team decode
@@ -1581,11 +1598,13 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
 static std::mutex g_team_mu;   // one team launch at a time per process: its grid must be resident as a whole
 
 static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* streams, const size_t* lens, int n_img,
-                         int Hb, int Wb, float* const* zhat, void* stream) {
+                         int Hb, int Wb, float* const* zhat, void* stream, bool after_timeout = false) {
     ms[0]->team_mode_last = 0;
     for (int t = 0; t < T; ++t) {
+        ms[t]->no_one = after_timeout;
         const int rc = lbc_decode(ms[t], streams + (size_t)t * n_img, lens + (size_t)t * n_img, n_img, Hb, Wb, zhat[t],
                                   stream);
+        ms[t]->no_one = false;
         if (rc) return rc;
     }
     return LBC_OK;
@@ -1666,13 +1685,10 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     // most tiles per workgroup over the step's GEMMs (the partials' LDS; the slower path needs 2)
     a.ni_max = 2;
     a.tab16 = rans[0].total16;
-    m0->team_ll_max = 0;
     for (const GemmArgs& d : gem) {
         const int items = ((d.M + 15) >> 4) * ((d.N + 15) >> 4);
         if (!team_fast_path(d, S)) continue;
         a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
-        const int nkb = d.K >> 4;
-        m0->team_ll_max = std::max(m0->team_ll_max, nkb / KSPLIT + (nkb % KSPLIT ? 1 : 0));
     }
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
     // before it run beside the rANS decode when every workgroup takes the fast path for it
@@ -1735,8 +1751,9 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // 768x768 frame, profiles/r04/r04_c5_b1_s*.log)
         const int rc1 = lbc_decode(ms[0], streams, lens, 1, Hb, Wb, zhat_devs[0], stream);
         if (rc1) return rc1;
-        ms[0]->team_mode_last = ms[0]->dec_path_last == 1 ? 3 : 0;
+        ms[0]->team_mode_last = ms[0]->dec_path_last == 1 ? 3 : 4;
         ms[0]->team_launch_bytes = ms[0]->team_launch_flops = 0;
+        ms[0]->team_plain_last = -1;    // no team launch: lbc_team_stats reports the decode's own events (ev[2..3])
         return LBC_OK;
     }
     const int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
@@ -1786,13 +1803,9 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory
         a.dense = sparse ? 0 : 1;
-        // the weight ring (team.hip), opt-in (LBIC_TEAM_RING=1): whatever LDS one workgroup per CU leaves.  Measured
-        // slower than the register-prefetch path, so not the default
-        const char* rge = getenv("LBIC_TEAM_RING");
-        a.ring_q = !(rge && atoi(rge) == 1) || wpc > 1 ? 0 : team_ring_slots(a, m0->team_ll_max, 160 * 1024);
         const size_t lds = team_lds_bytes(a);
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
-        const int nb = team_blocks_per_cu(a.dense, a.ring_q > 0, lds);
+        const int nb = team_blocks_per_cu(a.dense, lds);
         if (nb >= wpc) break;
         if (nb < 1 || wpc == 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         wpc = nb;
@@ -1842,12 +1855,11 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         const char* ev = getenv("LBIC_TEAM_VERBOSE");
         if (!noted.exchange(true) || (ev && atoi(ev)))
             fprintf(stderr, "[lbic] team decode: barrier timeout, decoding through lbc_decode (counted: lbc_team_events)\n");
-        return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
+        return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream, true);
     }
     if (fail)   // any other failure word is a protocol error, not a residency problem: report it
         return set_error(LBC_E_STATE, "team decode: unexpected failure word " + std::to_string(fail));
     m0->team_plain_last = a.plain;
-    m0->team_ring_last = a.ring_q;
     m0->team_mode_last = a.dense == 1 ? 2 : 1;
     m0->team_launch_bytes = m0->team_step_bytes * T * Hb * Wb;
     m0->team_launch_flops = m0->team_step_flops * T * Hb * Wb;
@@ -1863,7 +1875,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
         fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d\n", T, S, a.plain, m0->team_fallbacks);
     for (int t = 0; t < T; ++t)
-        if ((rc = check_status(ms[t], (size_t)n_img, s))) return rc;
+        if ((rc = check_status(ms[t], (size_t)n_img, s, true))) return rc;
     return LBC_OK;
 }
 
@@ -1890,12 +1902,6 @@ int lbc_decode_path(const lbc_model* m, int* path, int* timeouts) {
     if (!m || !path || !timeouts) return set_error(LBC_E_ARG, "null argument");
     *path = m->dec_path_last;
     *timeouts = m->one_timeouts;
-    return LBC_OK;
-}
-
-int lbc_team_ring(const lbc_model* m, int* slots) {
-    if (!m || !slots) return set_error(LBC_E_ARG, "null argument");
-    *slots = m->team_ring_last;
     return LBC_OK;
 }
 
@@ -2019,7 +2025,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
         }
         m->prof.active = false;
         m->prof.nochain = false;
-        m->prof.used0 = m->prof.next;
+        // (used0 counts the ENCODER graph's range-0 slots: set by lbc_encode_ex's capture only -- ADVICE r4)
         g_prof = nullptr;
         hipGraph_t graph = nullptr;
         const hipError_t e = hipStreamEndCapture(m->cap, &graph);
@@ -2038,7 +2044,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
     if ((rc = launch_copy_interior(m->zpad.as<float>(), zhat_dev, n_img, Hb, Wb, m->Cx, s))) return rc;
     HIPCHK(hipEventRecord(m->ev[3], s));
     m->dec_timed = true;
-    return check_status(m, subs.size(), s);
+    return check_status(m, subs.size(), s, true);
 }
 
 int lbc_profile_begin(lbc_model* m, int sample_every) {
@@ -2078,7 +2084,7 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
     Prof& p = m->prof;
     lbc_kernel_stat acc[4];
     std::memset(acc, 0, sizeof(acc));
-    for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", kKernelNames[c]);
+    for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", c == 1 ? encoder_gemm_name() : kKernelNames[c]);
     if (p.slots && !p.recs.empty()) {
         HIPCHK(hipDeviceSynchronize());
         std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * kRanges);

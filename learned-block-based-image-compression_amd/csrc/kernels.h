@@ -131,8 +131,6 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team P: 1, 2, 4 or 8 (T <= 8 / P: team t = the workgroups on slots P t ..
                              // P t + P - 1, S ranks over P XCDs; P > 1: hand-offs write-through, plain = 0)
-    int ring_q;              // > 0: the weight-ring instance (team.hip): loader waves stream every fast-path GEMM's
-                             // weights into 8 LDS rings of ring_q 1-KB slots; 0: the computing waves load them
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {
@@ -202,12 +200,11 @@ int launch_dec_one(const OneArgs& a, int grid, hipStream_t s);
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch
 size_t team_lds_bytes(const TeamArgs& a);   // k_dec_team's dynamic LDS for a launch
 int launch_dec_team(const TeamArgs& a, hipStream_t s);
-int team_blocks_per_cu(int dense, int ring, size_t lds);   // k_dec_team workgroups one CU holds at `lds` bytes of
-                                                          // dynamic LDS (occupancy query; 0 on error)
-int team_threads(int ring);                      // threads per k_dec_team workgroup
-int team_ring_slots(const TeamArgs& a, int ll_max, size_t lds_budget);   // ring slots per K slice that fit (0: none)
+int team_blocks_per_cu(int dense, size_t lds);   // k_dec_team workgroups one CU holds at `lds` bytes of dynamic LDS
+                                                 // (occupancy query; 0 on error)
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
-int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = k_gemm
+int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = the encoder's GEMM
+const char* encoder_gemm_name();     // class 1's kernel: "k_gemm_t" (LDS-staged, the default) or "k_gemm"
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s);

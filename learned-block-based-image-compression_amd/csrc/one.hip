@@ -210,6 +210,11 @@ __device__ __forceinline__ bool one_gemm(const OneArgs& a, const OneOp& op, int 
         }
         cb = ce;
     }
+    // a row start (h = 0): the context net's first op has no left tap, so nothing above orders it after the previous
+    // step.  Wait for d3 of step t - 1 (every op of step t - 1 done, so every reader of a granule has read it) before
+    // this step's granules overwrite any: without it the new row's ops could republish while a slow
+    // consumer of step t - 1 still polls for the old tag -- correct values, but a stall until the timeout
+    if (o == 0 && h == 0 && t >= 1 && wave == 0) zneed = max(zneed, (unsigned)t);
     if (zneed && ok) {
         for (int g0 = 0; g0 < last.gw && ok; g0 += 256)
             ok = wave_wait_gran(last.gran, g0, min(256, last.gw - g0), zneed, scr + 240, c, true);

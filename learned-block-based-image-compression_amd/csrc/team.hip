@@ -4,7 +4,7 @@
 namespace lbic {
 
 constexpr int RC_WORDS = 576;   // rans_row_sparse's persistent coder-state cache (see kernels_dev.h)
-constexpr int CTL_WORDS = 32;   // LDS control words of the weight ring (below)
+constexpr int CTL_WORDS = 32;   // LDS control words (word 18: the barrier verdict team_sync broadcasts)
 
 // ----------------------------------------------------------------------------------------- team decoder
 // k_dec_team: the reference-format raster decodes of T <= 8 batches in ONE persistent launch.  Team t = the S
@@ -39,196 +39,17 @@ __device__ __forceinline__ f4 small_a_sc1(const SRow& rw, int kb) {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (o + (unsigned)(k >> 2)) << 4, 0, 16));
 }
 
-// ----------------------------------------------------------------------------------------- the weight ring
-// The RING instance of k_dec_team streams every GEMM's weights through LDS: TEAM_NLD loader waves per workgroup walk the
-// whole launch's sequence of weight fragments -- the recorded raster step's GEMMs, this workgroup's output tiles, every
-// K slice -- and copy them into per-slice rings in LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB, one k-block of one
-// column tile, per wave instruction, no registers), running ahead of the computing waves across team barriers, the
-// rANS decode and raster steps, as far as the rings allow.  The eight computing waves (one K slice each, as before)
-// read their weight fragments from their slice's ring (ds_read_b128) instead of from global memory; the A operand, the
-// arithmetic and the reduction are unchanged, so results stay bit-identical.  (MI355X_MICROARCH.md "ldsdma-fill",
-// "ring-gemm", "prefetch-credit": a CU's weight intake is bounded by the loads it keeps in flight; DMA into LDS keeps
-// them in flight without registers and across the barriers, where the computing waves have nothing to load.)
-//   ring s (slice s): Q slots of 1 KB = 64 f4; unit u of the slice's sequence lives in slot u % Q.
-//   ctl[s] FULL: units of slice s landed (loader), ctl[8 + s] FREE: units of slice s consumed (computing wave s),
-//   ctl[16] abort (a computing wave leaves early: the loaders stop), ctl[17] the computing waves' barrier counter,
-//   ctl[18] the barrier flag of team_sync.
-// Loader order = the computing waves' consumption order (GEMM by GEMM, item by item; for the GEMM split around the rANS
-// decode first the slices computed beside it, then the others), and a loader publishes everything it has issued
-// before it ever waits for ring space: so no computing wave waits for a unit its loader can only issue after that wave
-// has moved on, i.e. no deadlock for any ring size >= one item's slice.
-// The computing waves cannot use s_barrier (it counts the loader waves too): they meet at an LDS counter (cbar).
-#ifndef LBIC_TEAM_NLD
-#define LBIC_TEAM_NLD 4
-#endif
-constexpr int TEAM_NLD = LBIC_TEAM_NLD;   // loader waves per workgroup (MI355X_MICROARCH.md "ring-gemm": 4 loaders beat 1-2)
-constexpr int TEAM_LAG = 12;              // units a loader keeps in flight past the last published one
-
-// LDS accesses of the loader waves as inline asm: the compiler waits vmcnt(0) (draining every DMA in flight) before any
-// LDS access it can see while an LDS-DMA is pending; these it cannot see
-__device__ __forceinline__ unsigned lds_off(const void* p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ unsigned lds_ld_asm(const uint32_t* p) {
-    unsigned v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off(p)) : "memory");
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void lds_st_asm(uint32_t* p, unsigned v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
-}
-// a computing wave's view of its slice's ring
-struct RingC {
-    const f4* slots;     // ring of this wave's slice: Q x 64 f4
-    uint32_t* ctl;
-    int Q;
-    unsigned pos;        // units of this slice consumed so far
-    unsigned full;       // last FULL value read
-    unsigned long long tmo;
-    unsigned* fail;
-};
-
-// the computing waves' barrier (waves 0..7 of a RING workgroup): LDS stores before it are visible after it
-__device__ __forceinline__ void cbar(uint32_t* ctl, unsigned& ep) {
-    ep += KSPLIT;
-    asm volatile("" ::: "memory");
-    if ((threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_add(ctl + 17, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(ctl + 17, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ep) {
-    }
-    asm volatile("" ::: "memory");
-}
-
-template <bool RING>
-__device__ __forceinline__ void wg_bar(uint32_t* ctl, unsigned& ep) {
-    if constexpr (RING) {
-        cbar(ctl, ep);
-    } else {
-        (void)ctl; (void)ep;
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-    }
-}
-
-// the computing wave waits until the ring holds units [pos, need) of its slice (bounded: a timeout sets the failure
-// word and stops waiting -- the launch is then discarded by the host)
-__device__ __forceinline__ void ring_wait(RingC& rg, unsigned need) {
-    if (rg.full >= need) return;
-    const int wave = threadIdx.x >> 6;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        rg.full = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(rg.ctl + wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (rg.full >= need) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > rg.tmo) {
-            if ((threadIdx.x & 63) == 0)
-                __hip_atomic_store((gptr<unsigned>)rg.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rg.full = ~0u;    // results of this launch are discarded; never wait again
-            break;
-        }
-        __builtin_amdgcn_s_sleep(0);
-    }
-    asm volatile("" ::: "memory");   // the slot reads stay below the poll
-}
-
-// one loader wave: slices l, l + TEAM_NLD, ... of every ring GEMM of every raster step, in the computing waves' order.
-// Publication: every unit issued is recorded (slice, position) in one lane of a history register (64 entries); once
-// more than TEAM_LAG units are in flight the wave waits until only TEAM_LAG are (s_waitcnt vmcnt) and publishes the
-// oldest entries -- FULL trails the issue by TEAM_LAG units, whatever the GEMM's shape.  Before it ever waits for ring
-// space it waits for everything and publishes it all.
-__device__ __forceinline__ void team_loader(const TeamArgs& ta, const GemmArgs* G, int rank, int S, uint32_t* ctl,
-                                            f4* ring, int Q, int l) {
-    constexpr int NS = KSPLIT / TEAM_NLD;     // slices per loader
-    const int lane = threadIdx.x & 63;
-    unsigned wpos[NS], freec[NS], slot[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) wpos[i] = freec[i] = slot[i] = 0u;
-    int hist = 0;                             // lane k: (slice << 29) | (position + 1) of the unit issued k (mod 64)
-    int issued = 0, pubd = 0;
-    bool dead = false;
-    auto publish_one = [&]() {
-        const unsigned e = (unsigned)__builtin_amdgcn_readlane(hist, pubd & 63);
-        if (lane == 0) lds_st_asm(ctl + (e >> 29), e & 0x1fffffffu);
-        ++pubd;
-    };
-    auto publish_all = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        while (pubd < issued) publish_one();
-    };
-    // the units of slice s = l + i NLD of one item (column tile nt) of GEMM g
-    auto issue = [&](const GemmArgs& g, int i, int nt) {
-        const int s = l + i * TEAM_NLD, nkb = g.K >> 4;
-        const int kb0 = s * nkb / KSPLIT, n = (s + 1) * nkb / KSPLIT - kb0;
-        const f4* src = reinterpret_cast<const f4*>(g.W) + ((long)kb0 * g.NB16 + nt) * 64 + lane;
-        const long step = (long)g.NB16 * 64;
-        f4* rs = ring + (long)s * Q * 64;
-        for (int c = 0; c < n; ++c) {
-            if (wpos[i] >= freec[i] + (unsigned)Q) {       // ring full: wait for the computing wave
-                freec[i] = lds_ld_asm(ctl + 8 + s);
-                if (wpos[i] >= freec[i] + (unsigned)Q) {
-                    publish_all();                          // (everything it may be waiting for)
-                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                    for (;;) {
-                        __builtin_amdgcn_s_sleep(1);
-                        freec[i] = lds_ld_asm(ctl + 8 + s);
-                        if (wpos[i] < freec[i] + (unsigned)Q) break;
-                        if (lds_ld_asm(ctl + 16) || __builtin_amdgcn_s_memrealtime() - t0 > ta.tmo) {
-                            dead = true;
-                            return;
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_global_load_lds((const void*)(src + c * step),
-                                             (__attribute__((address_space(3))) void*)(rs + slot[i] * 64), 16, 0, 0);
-            ++wpos[i];
-            slot[i] = slot[i] + 1 == (unsigned)Q ? 0u : slot[i] + 1;
-            hist = lane == (issued & 63) ? (int)(((unsigned)s << 29) | wpos[i]) : hist;
-            ++issued;
-            if (issued - pubd > TEAM_LAG) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TEAM_LAG) : "memory");
-                while (issued - pubd > TEAM_LAG) publish_one();
-            }
-        }
-    };
-    typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
-    const cgemm_p Gc = (cgemm_p)G;
-    for (int v = 0; v < ta.Hb && !dead; ++v) {
-        for (int h = 0; h < ta.Wb && !dead; ++h) {
-            const int cls = h == 0 ? 0 : h == ta.Wb - 1 ? 2 : 1;
-            for (int op = 0; op < ta.nops && !dead; ++op) {
-                const int k = ta.opk[op];
-                if (k < 0) continue;
-                const GemmArgs& g = *(const GemmArgs*)(Gc + cls * ta.NG + k);
-                if (!team_fast_path(g, S)) continue;          // team_gemm_long reads its weights itself
-                const int MT = (g.M + 15) >> 4, items = MT * ((g.N + 15) >> 4);
-                const int ni = rank < items ? (items - rank + S - 1) / S : 0;
-                const bool split = op == ta.split_op;
-                for (int pass = 0; pass < (split ? 2 : 1) && !dead; ++pass) {
-                    for (int j = 0; j < ni && !dead; ++j) {
-                        const int nt = (rank + j * S) / MT;
-#pragma unroll
-                        for (int i = 0; i < NS; ++i) {
-                            const int s = l + i * TEAM_NLD;
-                            // the split GEMM: slices < wy (computed beside the rANS decode) first, then the rest
-                            if (split && ((pass == 0) != (s < ta.split_wy))) continue;
-                            if (!dead) issue(g, i, nt);
-                        }
-                    }
-                }
-            }
-        }
-    }
-    if (!dead) publish_all();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// the workgroup's barrier between the partial stores to LDS and the reduction
+__device__ __forceinline__ void wg_bar() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
 }
 
 // K beyond the fast path (or more than two row tiles): each output tile (row tile mt, column tile nt) = item
 // i = nt * MT + mt, items rank, rank + S, ...; each item's slice in chunks of CH k-blocks, double-buffered: chunk c + 1's
 // fragments are requested before chunk c's MFMAs (the KS3311 context layer 1, K = 5 C1, streams 8-67 k-blocks per slice)
-template <bool RING>
 __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ntn, float* red,
-                                               bool wt, uint32_t* ctl, unsigned& ep) {
+                                               bool wt) {
     constexpr int CH = 4;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -287,7 +108,7 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
         buf ^= 1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) rb[wave * 256 + i * 64 + lane] = acc[i];
-        wg_bar<RING>(ctl, ep);
+        wg_bar();
         if (threadIdx.x < 256) {
             const int e = threadIdx.x;
             float vv = rb[e];
@@ -323,10 +144,9 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 #endif
 }
 
-template <int L, bool EXACT, bool SQ, bool RING>
+template <int L, bool EXACT, bool SQ>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
-                                                float* red, bool wt, int ph, int wy, unsigned long long* dts, RingC& rg,
-                                                unsigned& ep) {
+                                                float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
     constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
     constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
@@ -358,27 +178,9 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     if (act) {      // loads and chains in one branch: no join between a load and its use
         f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
-            if constexpr (RING) {
-                // units pos .. pos + n - 1 of this wave's ring (item j's k-blocks kb0 .. kb0 + n - 1); an (L+1)-th
-                // fragment of a shorter slice repeats the last (its MFMAs are discarded below)
-                const unsigned need = rg.pos + (unsigned)n;
-                ring_wait(rg, need);
-                const int s0 = (int)(rg.pos % (unsigned)rg.Q);
+            const int nt = nt0 + (rank + j * S) / MT;
 #pragma unroll
-                for (int c = 0; c < LL; ++c) {
-                    int u = s0 + min(c, n - 1);
-                    u = u >= rg.Q ? u - rg.Q : u;
-                    w[c] = rg.slots[u * 64 + lane];
-                }
-                asm volatile("" ::: "memory");       // (LDS executes a wave's accesses in order: the slots are read
-                if (lane == 0)                       // before the loader can see them freed)
-                    __hip_atomic_store(rg.ctl + 8 + wave, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                rg.pos = need;
-            } else {
-                const int nt = nt0 + (rank + j * S) / MT;
-#pragma unroll
-                for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
-            }
+            for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
         };
         auto chain = [&](int j, f4 (&w)[LL]) {
             __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
@@ -411,14 +213,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         dstamp(dts, 1, 0.f);
         // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
         // hit) so that no load sits behind a branch
-        if constexpr (RING) {
-            // the next item's fragments come from LDS (short latency) once its chain is issued
-            for (int j = 0;;) {
-                chain(j, w0);
-                if (++j >= ni) break;
-                issue(j, w0);
-            }
-        } else if constexpr (PF) {
+        if constexpr (PF) {
             for (int j = 0;;) {
                 issue(min(j + 1, ni - 1), w1);
                 chain(j, w0);
@@ -436,7 +231,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         }
     }
     if (ph == 1) return;
-    wg_bar<RING>(rg.ctl, ep);
+    wg_bar();
 #pragma unroll
     for (int q = 0; q < NOMAX; ++q) {
         const int o = threadIdx.x + 512 * q;
@@ -453,9 +248,8 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 }
 
 // The output tiles of g this workgroup computes: rank `rank` of the team's S workgroups
-template <bool RING>
 __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
-                                              int ph, int wy, unsigned long long* dts, RingC& rg, unsigned& ep) {
+                                              int ph, int wy, unsigned long long* dts) {
     const int nt0 = 0, ntn = (g.N + 15) >> 4;
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
@@ -467,12 +261,12 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                          \
     case L_ * 2 + 1:                                                                                        \
-        if (g.square_a) team_gemm_items<L_, true, true, RING>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, rg, ep); \
-        else team_gemm_items<L_, true, false, RING>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, rg, ep);          \
+        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);          \
         return;                                                                                             \
     case L_ * 2:                                                                                            \
-        if (g.square_a) team_gemm_items<L_, false, true, RING>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, rg, ep); \
-        else team_gemm_items<L_, false, false, RING>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, rg, ep);         \
+        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);         \
         return;
             LBIC_N(1) LBIC_N(2) LBIC_N(3) LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
@@ -480,18 +274,15 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
         }
     }
     if (ph == 1) return;     // (the host splits a GEMM only where every workgroup takes the path above)
-    team_gemm_long<RING>(g, v, h, rank, S, nt0, ntn, red, wt, rg.ctl, ep);
+    team_gemm_long(g, v, h, rank, S, nt0, ntn, red, wt);
 }
 
 // team barrier: every wave's stores drained, one arrival per workgroup, one lane polls (relaxed, s_sleep between
-// polls, bounded); false: the launch failed (timeout here or anywhere else).  RING: the computing waves meet at their
-// LDS barrier (the loader waves never take part)
-template <bool RING>
+// polls, bounded); false: the launch failed (timeout here or anywhere else)
 __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsigned* fail, unsigned long long tmo,
-                                          int* sflag, uint32_t* ctl, unsigned& ep) {
+                                          int* sflag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave (R1)
-    if constexpr (RING) cbar(ctl, ep);
-    else __syncthreads();
+    __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_fetch_add((gptr<unsigned>)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) {
@@ -512,8 +303,7 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
         }
         *sflag = f;
     }
-    if constexpr (RING) cbar(ctl, ep);
-    else __syncthreads();
+    __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the poll
     return *sflag == 0;
 }
@@ -524,14 +314,13 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // relaunches with plain = 0 (every hand-off write-through): results never depend on placement.
 // 128 VGPRs at most (4 waves per SIMD): the encoder's kernels keep room beside the persistent launch.
 // DENSE (TeamArgs::dense): the high-rate instance, tables staged in LDS and rans_row<true>; a separate instance so the
-// low-rate one keeps its register allocation.  RING (TeamArgs::ring_q > 0): TEAM_NLD more waves per workgroup stream
-// the weights into LDS rings (above).
-template <bool DENSE, bool RING>
-__global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_team(const TeamArgs ta) {
+// low-rate one keeps its register allocation.
+template <bool DENSE>
+__global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // dynamic LDS, sized by the host (team_lds_bytes):
     // [rANS window RANS_WIN words][rANS cache RC_WORDS words][control CTL_WORDS words][rANS centre intervals 256 words]
     // [GEMM partials ni_max x KSPLIT x 256 floats]
-    // [dense rANS only: the table image, total16 16-bit entries]  [RING only: 8 rings x ring_q x 1 KB]
+    // [dense rANS only: the table image, total16 16-bit entries]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
     uint32_t* lwin = team_lds;
     uint32_t* rcache = team_lds + RANS_WIN;                              // rans_row_sparse<.., true>'s state cache
@@ -539,9 +328,7 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
     int& sflag = *reinterpret_cast<int*>(ctl + 18);
     uint32_t* llf = team_lds + RANS_WIN + RC_WORDS + CTL_WORDS;          // rans_row_sparse's vector runs
     float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + CTL_WORDS + 256);
-    f4* ring = reinterpret_cast<f4*>(red + ta.ni_max * KSPLIT * 256);
     if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
-    if (RING && threadIdx.x < CTL_WORDS) ctl[threadIdx.x] = 0u;
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
@@ -571,18 +358,7 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
         uint4* dst = reinterpret_cast<uint4*>(tab);
         for (int i = threadIdx.x; i < R.total16 / 8; i += blockDim.x) dst[i] = src[i];
     }
-    __syncthreads();      // (the last barrier of every wave: the loader waves leave the computing waves here)
-    if constexpr (RING) {
-        if (wave >= KSPLIT) {
-            team_loader(ta, (const GemmArgs*)G, rank, S, ctl, ring, ta.ring_q, wave - KSPLIT);
-            return;
-        }
-    }
-    RingC rg{ring + (long)wave * ta.ring_q * 64, ctl, ta.ring_q, 0u, 0u, ta.tmo, fail};
-    unsigned ep = 0;         // the computing waves' LDS barrier count (RING)
-    auto leave = [&]() {     // an early exit: the loaders stop too
-        if (RING && threadIdx.x == 0) __hip_atomic_store(ctl + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
+    __syncthreads();
     unsigned target = 0;
     const bool wt = !ta.plain;
     if (ta.plain) {
@@ -591,14 +367,14 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
         if (threadIdx.x == 0)
             __hip_atomic_fetch_or((gptr<unsigned>)(ta.sync + team * 32 + 1), 1u << xcc_id(), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
-        if (!team_sync<RING>(ta.sync + T * 32 + 1, (unsigned)(T * S), fail, ta.tmo, &sflag, ctl, ep)) return leave();
+        if (!team_sync(ta.sync + T * 32 + 1, (unsigned)(T * S), fail, ta.tmo, &sflag)) return;
         bool local = true;
         for (int t = 0; t < T; ++t)
             local &= __popc(__hip_atomic_load((gptr<unsigned>)(ta.sync + t * 32 + 1), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT)) == 1;
         if (!local) {
             if (threadIdx.x == 0) __hip_atomic_store((gptr<unsigned>)fail, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return leave();
+            return;
         }
     }
     for (int v = 0; v < ta.Hb; ++v) {
@@ -609,8 +385,8 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
                 const int k = ta.opk[op];
                 if (k >= 0) {
                     const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + k);
-                    team_gemm_any<RING>(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
-                                        samp ? ts + 64 + op * 8 : nullptr, rg, ep);
+                    team_gemm_any(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
+                                  samp ? ts + 64 + op * 8 : nullptr);
                 } else {
                     // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
                     // the next GEMM (the decoder's first layer) that do not read y_qnt
@@ -630,13 +406,13 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
                         if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
-                        team_gemm_any<RING>(g, v, h, rank, S, red, wt, 1, ta.split_wy, nullptr, rg, ep);
+                        team_gemm_any(g, v, h, rank, S, red, wt, 1, ta.split_wy, nullptr);
                         if (sstep && threadIdx.x == 0) tsr[192 + rank] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
                 if (samp && threadIdx.x == 0) ts[32 + op] = __builtin_amdgcn_s_memrealtime();
                 target += S;
-                if (!team_sync<RING>(ctr, target, fail, ta.tmo, &sflag, ctl, ep)) return leave();
+                if (!team_sync(ctr, target, fail, ta.tmo, &sflag)) return;
                 if (samp && threadIdx.x == 0) ts[op] = __builtin_amdgcn_s_memrealtime();
             }
             if (samp && threadIdx.x == 0) ts[61] = __builtin_amdgcn_s_memrealtime();
@@ -646,48 +422,30 @@ __global__ __launch_bounds__(RING ? 512 + 64 * TEAM_NLD : 512, 4) void k_dec_tea
     if (ts && threadIdx.x == 0) ts[63] = __builtin_amdgcn_s_memrealtime();
 }
 
-static const void* team_instance(int dense, int ring) {
-    return dense ? reinterpret_cast<const void*>(&k_dec_team<true, false>)
-           : ring ? reinterpret_cast<const void*>(&k_dec_team<false, true>)
-                  : reinterpret_cast<const void*>(&k_dec_team<false, false>);
+static const void* team_instance(int dense) {
+    return dense ? reinterpret_cast<const void*>(&k_dec_team<true>) : reinterpret_cast<const void*>(&k_dec_team<false>);
 }
 
-int team_threads(int ring) { return ring ? 512 + 64 * TEAM_NLD : 512; }
-
-int team_blocks_per_cu(int dense, int ring, size_t lds) {
+int team_blocks_per_cu(int dense, size_t lds) {
     int nb = 0;
-    const void* f = team_instance(dense, ring);
+    const void* f = team_instance(dense);
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, team_threads(ring), lds) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 512, lds) != hipSuccess) return 0;
     return nb;
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
     return (size_t)(RANS_WIN + RC_WORDS + CTL_WORDS + 256) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 +
-           (size_t)(a.dense ? 1 : 0) * a.tab16 * 2 + (size_t)a.ring_q * KSPLIT * 1024;
-}
-
-// the ring slots the LDS left after everything else holds (0: the ring does not apply -- dense rANS tables in LDS, or
-// fewer slots than one item's K slice needs)
-int team_ring_slots(const TeamArgs& a, int ll_max, size_t lds_budget) {
-    if (a.dense) return 0;
-    TeamArgs b = a;
-    b.ring_q = 0;
-    const size_t fixed = team_lds_bytes(b);
-    if (fixed >= lds_budget) return 0;
-    const int q = (int)std::min<size_t>((lds_budget - fixed) / (KSPLIT * 1024), 32);
-    return q >= std::max(ll_max, 1) ? q : 0;
+           (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
 int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
         return set_error(LBC_E_ARG, "bad team decoder arguments");
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
-    if (a.ring_q < 0 || (a.ring_q && a.dense)) return set_error(LBC_E_ARG, "bad team ring geometry");
     static const bool attr = [] {
-        for (int d = 0; d < 3; ++d)
-            (void)hipFuncSetAttribute(team_instance(d == 2, d == 1), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
+        for (int d = 0; d < 2; ++d)
+            (void)hipFuncSetAttribute(team_instance(d), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
@@ -697,9 +455,8 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
         (a.spread > 1 && (a.T > TEAM_MAX / a.spread || a.S % a.spread || a.plain)))
         return set_error(LBC_E_ARG, "bad team spread");
     const dim3 grid(8 * a.S / a.spread);
-    if (a.dense) hipLaunchKernelGGL((k_dec_team<true, false>), grid, dim3(512), lds, s, a);
-    else if (a.ring_q) hipLaunchKernelGGL((k_dec_team<false, true>), grid, dim3(512 + 64 * TEAM_NLD), lds, s, a);
-    else hipLaunchKernelGGL((k_dec_team<false, false>), grid, dim3(512), lds, s, a);
+    if (a.dense) hipLaunchKernelGGL((k_dec_team<true>), grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((k_dec_team<false>), grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");
 }
 

@@ -52,7 +52,6 @@ _SIGS = {
                         ctypes.c_int),
     "lbc_team_mode": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_team_events": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
-    "lbc_team_ring": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_decode_path": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "lbc_one_stamps": ([_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
                        ctypes.c_int),

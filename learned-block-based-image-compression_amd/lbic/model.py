@@ -242,10 +242,11 @@ class BlockBasedImgCompLossyNetv9:
 
     def team_stats(self):
         """The last decompress_teams launch led by this handle (lbc_team_stats): dict(launch_ms, bytes, flops,
-        plain, mode, sc1_reruns, timeout_fallbacks, ring_slots) -- its duration, algorithmic bytes / FLOPs, the hand-off store mode
-        it ran in, how the call decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant, or "fallback" to
-        lbc_decode per batch), and the handle's event counters (lbc_team_events): write-through reruns and barrier
-        timeouts decoded through the fallback; the weight-ring slots per K slice it ran with (lbc_team_ring, 0: none)."""
+        plain, mode, sc1_reruns, timeout_fallbacks) -- its duration, algorithmic bytes / FLOPs, the hand-off store mode
+        it ran in, how the call decoded (lbc_team_mode: "team_sparse" / "team_dense" rANS variant, "fallback" to
+        lbc_decode per batch, or for one batch of one image "one" / "graphs": lbc_decode's single-image decoder or its
+        row graphs), and the handle's event counters (lbc_team_events): write-through reruns and barrier timeouts
+        decoded through the fallback."""
         L = _lib.lib()
         ms, by, fl, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         _lib.check(L.lbc_team_stats(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(fl), ctypes.byref(pl)))
@@ -253,11 +254,9 @@ class BlockBasedImgCompLossyNetv9:
         _lib.check(L.lbc_team_mode(self._h, ctypes.byref(mode)))
         rr, to = ctypes.c_int(), ctypes.c_int()
         _lib.check(L.lbc_team_events(self._h, ctypes.byref(rr), ctypes.byref(to)))
-        rq = ctypes.c_int()
-        _lib.check(L.lbc_team_ring(self._h, ctypes.byref(rq)))
         return dict(launch_ms=ms.value, bytes=by.value, flops=fl.value, plain=pl.value,
-                    mode=("fallback", "team_sparse", "team_dense", "one")[mode.value], sc1_reruns=rr.value,
-                    timeout_fallbacks=to.value, ring_slots=rq.value)
+                    mode=("fallback", "team_sparse", "team_dense", "one", "graphs")[mode.value], sc1_reruns=rr.value,
+                    timeout_fallbacks=to.value)
 
     def decode_path(self):
         """How the last decompress of this handle ran (lbc_decode_path): dict(path="graphs" | "one", one_timeouts) --

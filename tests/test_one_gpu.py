@@ -8,8 +8,10 @@ decompress() (graphs/models/BlockBasedImgCompLossy_net.py:400-452) as eval_model
 * Library-encoded frames of ragged shapes (one block row, one block column, two columns, odd sizes) decode bit-exactly
   to the encoder's reconstruction, through k_dec_one.
 * The full 768x768 B8_lowrate frame: tests/test_fullsize_gpu.py::test_full_frame_b8_lowrate_vs_reference decodes it as
-  one image, i.e. through k_dec_one (asserted there).
+  one image through k_dec_one (asserted there: ``decode_path()`` and no timeout).
 * A launch whose waits time out (LBIC_ONE_TMO=1 tick) is decoded by the row graphs instead, counted, same result.
+* Truncated and corrupted streams decoded through k_dec_one raise (an overrun, or a decode that does not end in the
+  encoder's initial rANS state), without a timeout, and the handle decodes correctly afterwards.
 * Geometries it does not cover (KS[1] = 3: the layer-0 cache; several images) keep the row graphs.
 """
 import types
@@ -112,3 +114,31 @@ def test_one_not_for_layer0_cache_or_batches():
     z = m.decompress_batch([stream, stream], Hb, Wb)
     assert m.decode_path()["path"] == "graphs"            # two images: the row graphs
     assert torch.equal(z[0], z[1])
+
+
+@pytest.mark.parametrize("damage", ["truncated", "corrupt_head", "corrupt_tail"])
+def test_one_bad_stream_raises(damage, monkeypatch):
+    """A damaged stream through k_dec_one (sparse rANS forced, so the low-rate kernel runs whatever the stream's rate):
+    the decode raises instead of returning a wrong image, no wait times out, and the handle still decodes."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    g = load_golden("loop_tiny_ks3111")
+    arch = golden_arch(g)
+    Hb, Wb = g["x"].shape[:2]
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
+    good = m.decompress_batch([stream], Hb, Wb)
+    assert m.decode_path()["path"] == "one"
+    w = bytearray(stream)
+    if damage == "truncated":
+        w = w[:len(w) // 2 - (len(w) // 2) % 4]
+    elif damage == "corrupt_head":                  # the initial coder state
+        w[0:4] = bytes(b ^ 0x5A for b in w[0:4])
+    else:                                           # a word the last blocks read
+        w[-4:] = bytes(b ^ 0xA5 for b in w[-4:])
+    t0 = m.decode_path()["one_timeouts"]
+    with pytest.raises((RuntimeError, ValueError)):
+        m.decompress_batch([bytes(w)], Hb, Wb)
+    p = m.decode_path()
+    assert p["path"] == "one" and p["one_timeouts"] == t0, p
+    assert torch.equal(m.decompress_batch([stream], Hb, Wb), good)
+    assert m.decode_path()["path"] == "one"

@@ -108,3 +108,30 @@ def test_bench_gather_records_gloo(tmp_path):
     rec = np.load(out)
     assert rec.shape == (4, 3)
     assert list(rec[:, 0]) == [100.0, 200.0, 101.0, 201.0]
+
+
+def test_bench_roofline_dominance_is_wall_occupancy():
+    """bench.py's roofline picks the dominant kernel by wall occupancy in the timed region: the team
+    decoder's summed launch durations against the encoder graphs' wall time -- not the encoder launches' summed
+    durations, which exceed the graphs' wall time because the forked branches overlap."""
+    import bench
+    dt, steps = 4.5, 20
+    # encoder: 100,000 launches of 50 us each (5.0 s summed) inside 3.5 s of graph wall time; team: 3 launches, 3.9 s
+    kstats = {"k_gemm_t": dict(launches=1000, total_launches=100000, total_ms=50.0, flops=1e12, bytes=9e9,
+                               total_flops=1e17, total_bytes=9e14),
+              "k_gemm_s": dict(launches=10, total_launches=500, total_ms=0.05, flops=1e9, bytes=1e8,
+                               total_flops=5e11, total_bytes=5e10)}
+    enc = dict(ms=3500.0, passes=20)
+    team = dict(launches=3, ms=3900.0, bytes=3 * 1.9e12, flops=3 * 2.8e13, steps=20 * 9216, plain=[1, 1, 1],
+                timeouts=0, hw=9216)
+    roof, kernels = bench.roofline(kstats, dt, team, enc, steps)
+    assert roof["kernel"] == "k_dec_team", roof
+    assert roof["wall_occupancy_ms_per_step"] <= dt / steps * 1e3      # the dominant kernel fits in the step
+    assert kernels["k_gemm_t"]["summed_launch_s"] > kernels["k_gemm_t"]["wall_occupancy_s"]
+    agg = roof["per_kernel"]["k_gemm_t"]["aggregate"]
+    assert abs(agg["achieved_tflops"] - (1e17 + 5e11) / 3.5 / 1e12) < 1e-2
+    assert abs(roof["achieved"] - 1.9e12 / 1.3 / 1e9) < 1.0 and roof["bound"] == "hbm"
+    # a faster decoder: the encoder graphs become the dominant family
+    team["ms"] = 2000.0
+    roof, _ = bench.roofline(kstats, dt, team, enc, steps)
+    assert roof["kernel"] == "k_gemm_t" and roof["bound"] == "mfma"

@@ -55,24 +55,21 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
     return ref, got, hs, st
 
 
-@pytest.mark.parametrize("ring", ["1", "0"])
 @pytest.mark.parametrize("name,T,n,shape", [
     ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
     ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)), ("b8_lowrate_2rows", 5, 48, (2, 9)),
     ("b8_lowrate_2rows", 8, 64, (2, 5)),
 ])
-def test_team_equals_graph_decoder(name, T, n, shape, ring, monkeypatch):
-    """Image counts of one, two, three and four row tiles, 1-8 teams; the weights streamed through the LDS rings by
-    loader waves (ring "1", LBIC_TEAM_RING=1, opt-in) or loaded by the computing waves (the default)."""
+def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
+    """Image counts of one, two, three and four row tiles, 1-8 teams."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
-    monkeypatch.setenv("LBIC_TEAM_RING", ring)
     g = load_golden("loop_" + name)
     Hb, Wb = shape or g["x"].shape[:2]
     ref, got, hs, _ = run_case(name, T, n, Hb, Wb, seed=T * 7 + n)
     for t in range(T):
         assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
     st = hs[0].team_stats()
-    assert st["mode"] == "team_sparse" and (st["ring_slots"] > 0) == (ring == "1"), st
+    assert st["mode"] == "team_sparse", st
 
 
 @pytest.mark.parametrize("name,T,n,shape", [("tiny_ks3311", 3, 5, (3, 4)), ("b8_lowrate_2rows", 4, 32, (2, 24))])

@@ -20,7 +20,7 @@ def main():
             gx = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
             wx = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)
             gy = int(r.get("Grid_Size_Y", 1) or 1)
-            fam = "k_gemm_s" if "k_gemm_s" in name else "k_gemm"
+            fam = "k_gemm_s" if "k_gemm_s" in name else "k_gemm_t" if "k_gemm_t" in name else "k_gemm"
             acc[(fam, gx // max(wx, 1), gy)].append(d)
             tot += d
     rows = sorted(acc.items(), key=lambda kv: -sum(kv[1]))
