@@ -730,17 +730,18 @@ def roofline(kstats, dt, team=None, enc=None, steps=0):
     kernels, fam = {}, {}
     if enc is not None and kstats:
         egm = "k_gemm_t" if "k_gemm_t" in kstats else "k_gemm"       # lbc_profile names the family by its kernel
-        n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
+        efam = (egm, "k_gemm", "k_gemm_s")      # every launch of the encoder graphs (k_gemm: the narrow-N layers)
+        n_all = sum(s["total_launches"] for k_, s in kstats.items() if k_ in efam)
         sg = kstats.get(egm, {})
         if n_all and enc["ms"] > 0:
             wall = enc["ms"] / n_all
-            tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
-            tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in (egm, "k_gemm_s"))
+            tf = sum(s["total_flops"] for k_, s in kstats.items() if k_ in efam)
+            tb = sum(s["total_bytes"] for k_, s in kstats.items() if k_ in efam)
             agg = dict(encoder_wall_s=round(enc["ms"] / 1e3, 4), encoder_graphs=enc["passes"],
                        tflop=round(tf / 1e12, 4), achieved_tflops=round(tf / (enc["ms"] / 1e3) / 1e12, 3),
                        frac=round(tf / (enc["ms"] / 1e3) / (PEAK_FP32_TFLOPS * 1e12), 5),
-                       note=f"every launch of the encoder graphs ({egm} + the k_gemm_s ramp steps): algorithmic FLOPs / "
-                            "the graphs' wall time")
+                       note=f"every launch of the encoder graphs ({', '.join(k_ for k_ in efam if k_ in kstats)}): "
+                            "algorithmic FLOPs / the graphs' wall time")
             if sg.get("launches"):
                 per = sg["total_ms"] / sg["launches"]
                 n_k = int(sg["total_launches"])

@@ -93,6 +93,8 @@ constexpr int kSlotU64 = 32;      // + per-phase max / sum / workgroup count (di
 constexpr int kSlotU64 = 16;      // 8 XCDs x {max(~start), max(end)}
 #endif
 constexpr int kRanges = 6;        // 0 encoder graph, 1..4 raster decoder lanes, 5 wavefront decoder graph
+// kernel classes of the profile: gemm_class() (0 k_gemm_s, 1 k_gemm), 2 rANS, 3 copies
+constexpr int kNClass = 4;
 struct Prof {
     int sample_every = 0;
     bool active = false;          // current step is sampled
@@ -103,8 +105,8 @@ struct Prof {
     int last_slot = -1;
     unsigned long long* slots = nullptr;   // device, kRanges ranges
     int range = 0, next = 0;               // slot allocation inside the range being captured
-    long long per_replay[8][4] = {};       // launches of each kernel class per replay of each range's graph
-    double work_replay[8][4][2] = {};      // their algorithmic FLOPs and bytes per replay (every launch, sampled or not)
+    long long per_replay[8][kNClass] = {};       // launches of each kernel class per replay of each range's graph
+    double work_replay[8][kNClass][2] = {};      // their algorithmic FLOPs and bytes per replay (every launch, sampled or not)
     long long replays[8] = {};             // replays of each range's graph since lbc_profile_begin
     bool nochain = false;                  // capturing a forked graph: no launch-to-launch period (two chains)
     // the encoder graph's slot range (0) copied to the host after EVERY replay since lbc_profile_begin (its stamps are
@@ -127,7 +129,7 @@ struct Prof {
         last_slot = slot;
     }
 };
-static const char* kKernelNames[] = {"k_gemm_s", "k_gemm", "k_rans_decode", "k_copy_interior"};
+static const char* kKernelNames[kNClass] = {"k_gemm_s", "k_gemm", "k_rans_decode", "k_copy_interior"};
 static thread_local Prof* g_prof = nullptr;
 
 struct HostT {
@@ -2082,9 +2084,10 @@ int lbc_profile_begin(lbc_model* m, int sample_every) {
 int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out) {
     if (!m || !out || !n_out) return set_error(LBC_E_ARG, "null argument");
     Prof& p = m->prof;
-    lbc_kernel_stat acc[4];
+    lbc_kernel_stat acc[kNClass];
     std::memset(acc, 0, sizeof(acc));
-    for (int c = 0; c < 4; ++c) snprintf(acc[c].name, sizeof(acc[c].name), "%s", c == 1 ? encoder_gemm_name() : kKernelNames[c]);
+    for (int c = 0; c < kNClass; ++c)
+        snprintf(acc[c].name, sizeof(acc[c].name), "%s", kKernelNames[c]);
     if (p.slots && !p.recs.empty()) {
         HIPCHK(hipDeviceSynchronize());
         std::vector<unsigned long long> h(kSlotU64 * (size_t)kSlotsPerRange * kRanges);
@@ -2158,7 +2161,7 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
         }
     }
     // true launch counts since lbc_profile_begin (the stamps are a sample of them)
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < kNClass; ++c) {
         long long tot = 0;
         for (int r = 0; r < 8; ++r) {
             tot += p.per_replay[r][c] * p.replays[r];
@@ -2168,7 +2171,7 @@ int lbc_profile_end(lbc_model* m, lbc_kernel_stat* out, int max_out, int* n_out)
         acc[c].total_launches = tot;
     }
     int n = 0;
-    for (int c = 0; c < 4 && n < max_out; ++c)
+    for (int c = 0; c < kNClass && n < max_out; ++c)
         if (acc[c].launches || acc[c].total_launches) out[n++] = acc[c];
     *n_out = n;
     return LBC_OK;

@@ -203,8 +203,7 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s);
 int team_blocks_per_cu(int dense, size_t lds);   // k_dec_team workgroups one CU holds at `lds` bytes of dynamic LDS
                                                  // (occupancy query; 0 on error)
 int launch_gemm(const GemmArgs& g, hipStream_t s, int* cfg_id = nullptr);   // cfg_id: 0 = k_gemm_s, 1 = k_gemm
-int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = the encoder's GEMM
-const char* encoder_gemm_name();     // class 1's kernel: "k_gemm_t" (LDS-staged, the default) or "k_gemm"
+int gemm_class(const GemmArgs& g);   // the kernel launch_gemm picks: 0 = k_gemm_s, 1 = k_gemm
 int launch_rans_decode(const RansArgs& a, hipStream_t s);
 int launch_ctr_add(int* ctr, int d, hipStream_t s);
 int launch_zero_u64(unsigned long long* p, int n, hipStream_t s);

@@ -127,207 +127,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     stamp_end(g.ts);
 }
 
-// ----------------------------------------------------------------------------------------- k_gemm_t
-// The encoder's wavefront GEMMs for N >= TG_MIN_N, LDS-staged: one 64 x 64 output tile per 512-thread workgroup.
-// Eight waves = two K groups x four spatial waves (each a 32 x 32 quarter, 2 x 2 MFMA subtiles): group 0 takes K
-// slices 0-3, group 1 slices 4-7.  Every operand fragment is brought into LDS once per group by LDS-DMA
-// (global_load_lds_dwordx4: one wave instruction = one 1-KB fragment in the MFMA operand layout, lane l's 16 bytes at
-// lane offset l, so the consumer's ds_read_b128 is lane-contiguous and conflict-free) and read by the two waves of the
-// group that share its row or column subtile: 16 FLOP per byte taken in by the CU, three times k_gemm's 16 x 32 tile,
-// whose waves each load their own fragments (5.3 FLOP/B: the CU's intake, not the MFMA pipe, bounded it).
-// Why two K groups: a tile is 204 of the ~256 workgroups of a typical wavefront step (1,031 rows x N = 768), so one
-// workgroup per CU; with four waves (one per SIMD) a wave's per-k-block overhead (the barrier, the DMA issue, the LDS
-// reads) cannot overlap its own MFMAs (in-order issue) -- measured 158-167 ms per batch against k_gemm's 94.  Two
-// groups put two waves on each SIMD and halve the serial k walk of a tile.
-// Arithmetic: each wave walks its group's K slices in k order; slice s's chain runs in `acc`
-// (v_mfma_f32_16x16x4_f32 on the same fragments, in the same order, as every other GEMM kernel).  Group 0 folds its
-// slices as it goes (F = p0, F += p1, p2, p3); group 1 keeps p4..p7; at the end F crosses to group 1 through LDS, which
-// folds ((((F + p4) + p5) + p6) + p7) -- the slice-ordered left fold the other kernels do through LDS (an empty slice
-// adds +0 there and here).  Results are therefore bit-identical to k_gemm / k_gemm_s / k_dec_team / k_dec_one.
-// Pipeline, per group: a ring of R one-k-block stages (8 fragments, 8 KB); every wave DMAs its row subtile's A fragment
-// and its column subtile's W fragment of each k-block (incremental source addresses; the A segment is looked up only
-// where one ends); per k-block: wait for its own DMAs (counted vmcnt), one s_barrier (everyone's landed, everyone done
-// reading the slot the next DMA overwrites), issue the k-block R - 1 ahead, read and multiply.  LDS reads are inline
-// asm: the compiler would otherwise drain every LDS-DMA in flight (vmcnt(0)) before any LDS read it can see.
-constexpr int TG_FRAG = 64;         // f4 per fragment (1 KB)
-constexpr int TG_R_DEFAULT = 4;     // k-block stages per group ring (R - 1 in flight): 2 x 32 KB of LDS
-constexpr int TG_MIN_N = 256;       // narrower GEMMs (N = 96 / 192: 2-3 column tiles, too few workgroups) stay on k_gemm
-
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// s_waitcnt vmcnt(2 n) for a wave-uniform n in [0, R - 2]: all but this wave's n youngest k-blocks landed
-template <int TG_R>
-__device__ __forceinline__ void tg_vmwait(int n) {
-    static_assert(TG_R - 2 <= 6, "vmcnt range");
-    switch (n) {
-#define LBIC_W(s)                                                                                          \
-    case s:                                                                                                \
-        if constexpr (s <= TG_R - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * s) : "memory");          \
-        break;
-        LBIC_W(1) LBIC_W(2) LBIC_W(3) LBIC_W(4) LBIC_W(5) LBIC_W(6)
-#undef LBIC_W
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
-template <bool SQ, int TG_R>
-__global__ __launch_bounds__(512) void k_gemm_t(const GemmArgs g) {
-    extern __shared__ __attribute__((aligned(16))) f4 tl[];   // [2 groups][TG_R][8 fragments: A 0-3, W 4-7][64]
-    warm_kernargs<10>();
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp = wave >> 2, wq = wave & 3;
-    const int wm = wq >> 1, wn = wq & 1;
-    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
-    stamp_start(g.ts);
-    const int4* bl = g.ctr ? g.blocks + (long)(*g.ctr) * g.ctr_stride : g.blocks;
-    const BlkSrc blocks{bl, 0, 0, 0, 0};
-    // this lane's DMA sources: A row m0 + 16 wq + lane % 16 (clamped), W column tile n0 / 16 + wq (clamped)
-    SRow rw;
-    {
-        const SBlk bk = small_blk<false>(g, m0 + 16 * wq, lane, blocks);
-        small_offsets(g, bk, lane, rw);
-    }
-    const int nkb = g.K >> 4;
-    const int kmid = 4 * nkb / KSPLIT;                         // group 0: k-blocks [0, kmid), group 1: [kmid, nkb)
-    const int kbA = grp ? kmid : 0, len = grp ? nkb - kmid : kmid;
-    const int L = max(kmid, nkb - kmid);                       // both groups meet at every barrier
-    const long wstep = (long)g.NB16 * TG_FRAG;
-    const f4* wp = reinterpret_cast<const f4*>(g.W) + (long)min((n0 >> 4) + wq, g.NB16 - 1) * TG_FRAG + lane +
-                   (long)kbA * wstep;
-    const f4* ap = nullptr;
-    int seg_end = -1;      // the first k-block past ap's segment (the A source is re-resolved there)
-    f4* ring = tl + grp * TG_R * 8 * TG_FRAG;
-    typedef __attribute__((address_space(3))) void* lds_vp;
-    auto issue = [&](int j) {         // k-block kbA + j into slot j % R (j ascending, one call per j)
-        const int kb = kbA + j;
-        if (kb >= seg_end) {
-            ap = small_a_ptr(rw, kb);
-            int e = nkb;
-#pragma unroll
-            for (int t = 1; t < MAXSEG; ++t) {
-                const int b = rw.k0[t] >> 4;
-                e = (b > kb && b < e) ? b : e;
-            }
-            seg_end = e;
-        }
-        f4* d = ring + (j % TG_R) * 8 * TG_FRAG;
-        __builtin_amdgcn_global_load_lds((const void*)ap, (lds_vp)(d + wq * TG_FRAG), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)wp, (lds_vp)(d + (4 + wq) * TG_FRAG), 16, 0, 0);
-        ap += 4;
-        wp += wstep;
-    };
-    const int pro = min(TG_R - 1, len);
-    for (int j = 0; j < pro; ++j) issue(j);
-
-    const unsigned lb = lds_addr(ring) + (unsigned)lane * 16;
-    const unsigned oa0 = (unsigned)(2 * wm) * 1024, oa1 = oa0 + 1024;
-    const unsigned ow0 = (unsigned)(4 + 2 * wn) * 1024, ow1 = ow0 + 1024;
-    // part[0]: group 0's running fold F; group 1: p4..p6 in part[0..2], p7 stays in acc
-    f4 part[3][2][2], acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            acc[i][jj] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 3; ++q) part[q][i][jj] = f4{0.f, 0.f, 0.f, 0.f};
-        }
-    int s = grp * 4;                       // the slice acc is accumulating
-    const int s_end = s + 4;
-    // close every slice of this group that ends at or before k-block `done`
-    auto close = [&](int done) {
-        while (s < s_end - grp && (s + 1) * nkb / KSPLIT <= done) {     // (group 1: slice 7 stays in acc)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    if (grp == 0) {
-                        part[0][i][jj] = s == 0 ? acc[i][jj] : part[0][i][jj] + acc[i][jj];
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q)
-                            if (s - 4 == q) part[q][i][jj] = acc[i][jj];
-                    }
-                    acc[i][jj] = f4{0.f, 0.f, 0.f, 0.f};
-                }
-            ++s;
-        }
-    };
-    close(kbA);
-    for (int j = 0; j < L; ++j) {
-        tg_vmwait<TG_R>(j < len ? min(len - 1 - j, TG_R - 2) : 0);
-        __builtin_amdgcn_s_barrier();
-        if (j + TG_R - 1 < len) issue(j + TG_R - 1);
-        if (j < len) {
-            const unsigned fb = lb + (unsigned)((j % TG_R) * 8 * 1024);
-            f4 a0, a1, w0, w1;
-            asm volatile(
-                "ds_read_b128 %0, %4\n\t"
-                "ds_read_b128 %1, %5\n\t"
-                "ds_read_b128 %2, %6\n\t"
-                "ds_read_b128 %3, %7\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(a0), "=&v"(a1), "=&v"(w0), "=&v"(w1)
-                : "v"(fb + oa0), "v"(fb + oa1), "v"(fb + ow0), "v"(fb + ow1)
-                : "memory");
-            if constexpr (SQ) {
-                a0 = a0 * a0;
-                a1 = a1 * a1;
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[e], w0[e], acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[e], w1[e], acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[e], w0[e], acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[e], w1[e], acc[1][1], 0, 0, 0);
-            }
-            close(kbA + j + 1);
-        }
-    }
-    close(nkb);
-    // F (group 0) -> group 1 through LDS (the rings are free once every wave passed the first barrier below); group 1
-    // folds in slice order and leaves the sums there; then all eight waves run the epilogue, eight elements a thread
-    float* xf = reinterpret_cast<float*>(tl);
-    __builtin_amdgcn_s_barrier();
-    const int xo = wq * 1024 + lane;       // element (i, jj, r) of this lane's quarter at xo + ((i 2 + jj) 4 + r) 64
-    if (grp == 0) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) xf[xo + ((i * 2 + jj) * 4 + r) * 64] = part[0][i][jj][r];
-    }
-    __syncthreads();
-    if (grp == 1) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = xf[xo + ((i * 2 + jj) * 4 + r) * 64];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) v += part[q][i][jj][r];
-                    xf[xo + ((i * 2 + jj) * 4 + r) * 64] = v + acc[i][jj][r];
-                }
-    }
-    __syncthreads();
-    const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-    for (int e = threadIdx.x; e < 4096; e += 512) {
-        const int l = e & 63, q = e >> 6;
-        const int r = q & 3, i = (q >> 3) & 1, jj = (q >> 2) & 1, qw = q >> 4;
-        const int row = m0 + 32 * (qw >> 1) + 16 * i + (l >> 4) * 4 + r;
-        const int col = n0 + 32 * (qw & 1) + 16 * jj + (l & 15);
-        if (row >= g.M || col >= g.N) continue;
-        epilogue(g, xf[e], row, col, blocks, g.bias[col], gdn ? g.gx[(long)row * g.ldx + col] : 0.f);
-    }
-    stamp_end(g.ts);
-}
-
 // k-blocks [kb0, kb0 + n) of this wave's slice onto acc; n in {L, L+1} (the 8 slices of nkb k-blocks
 // differ by at most one).  The (L+1)-th block is always loaded and multiplied into a side accumulator,
 // selected afterwards, so every load feeds an unconditional MFMA and none is sunk behind a branch.
@@ -443,17 +242,6 @@ constexpr int SMALL_MAX = 64, DEC_SMALL_MAX = 1024;
 int gemm_class(const GemmArgs& g) {
     return (g.M <= SMALL_MAX || (g.raster && g.M <= DEC_SMALL_MAX)) ? 0 : 1;
 }
-// the encoder's wavefront GEMM kernel: k_gemm_t with a ring of R k-block stages (default), or k_gemm (0)
-static int enc_tiled() {
-    static const int tiled = [] {
-        const char* e = getenv("LBIC_ENC_TILED");     // A/B switch: 0 = k_gemm; 4, 5, 6: k_gemm_t's ring depth
-        const int r = e ? atoi(e) : 0;   // (k_gemm_t is opt-in until it measures faster)
-        return r == 0 || r == 4 || r == 5 || r == 6 ? r : TG_R_DEFAULT;
-    }();
-    return tiled;
-}
-const char* encoder_gemm_name() { return enc_tiled() ? "k_gemm_t" : "k_gemm"; }
-
 template <int BM, int BN, int NW, int CH, int OCC = 1>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     const size_t lds = std::max<size_t>((size_t)KSPLIT * BM * BN * sizeof(float), (size_t)std::max(g.lds_floor, 0));
@@ -538,28 +326,6 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
         return launch_status("k_gemm_s");
     }
     if (cfg_id) *cfg_id = 1;
-    const int tiled = enc_tiled();
-    if (tiled && g.N >= TG_MIN_N) {
-        static const bool attr = [] {
-            for (const void* f : {reinterpret_cast<const void*>(&k_gemm_t<false, 4>), reinterpret_cast<const void*>(&k_gemm_t<true, 4>),
-                                  reinterpret_cast<const void*>(&k_gemm_t<false, 5>), reinterpret_cast<const void*>(&k_gemm_t<true, 5>),
-                                  reinterpret_cast<const void*>(&k_gemm_t<false, 6>), reinterpret_cast<const void*>(&k_gemm_t<true, 6>)})
-                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            return true;
-        }();
-        (void)attr;
-        const size_t lds = std::max<size_t>((size_t)2 * tiled * 8 * TG_FRAG * 16, (size_t)std::max(g.lds_floor, 0));
-        if (lds > 160 * 1024) return set_error(LBC_E_ARG, "LDS request above 160 KB");
-        dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
-#define LBIC_T(R)                                                                                  \
-    case R:                                                                                        \
-        if (g.square_a) hipLaunchKernelGGL((k_gemm_t<true, R>), grid, dim3(512), lds, s, g);       \
-        else hipLaunchKernelGGL((k_gemm_t<false, R>), grid, dim3(512), lds, s, g);                 \
-        break;
-        switch (tiled) { LBIC_T(5) LBIC_T(6) default: LBIC_T(4) }
-#undef LBIC_T
-        return launch_status("k_gemm_t");
-    }
     // Encoder wavefront steps (n_img images x up to 48 blocks): many small tiles beat few large ones; the per-tile K
     // loop is latency-bound, so the step wants workgroups and waves.  Measured encode time per 32-frame 768x768
     // batch, encoder alone (tools/enc_exp.py, profiles/r02_exp/encoder_occupancy.txt), every shape bit-identical:

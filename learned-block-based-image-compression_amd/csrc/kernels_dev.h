@@ -376,20 +376,6 @@ __device__ __forceinline__ f4 small_a(const SRow& rw, int kb) {
     return reinterpret_cast<const f4 __attribute__((address_space(1)))*>(base)[o + (unsigned)(k >> 2)];
 }
 
-// the address small_a loads from (k_gemm_t's LDS-DMA source)
-__device__ __forceinline__ const f4* small_a_ptr(const SRow& rw, int kb) {
-    const int k = kb << 4;
-    gfloat_p base = rw.base[0];
-    unsigned o = rw.off[0];
-#pragma unroll
-    for (int t = 1; t < MAXSEG; ++t) {
-        const bool in = k >= rw.k0[t];
-        base = in ? rw.base[t] : base;
-        o = in ? rw.off[t] : o;
-    }
-    return reinterpret_cast<const f4*>((const float*)base) + (o + (unsigned)(k >> 2));
-}
-
 #ifndef LBIC_RANS_WPB
 #define LBIC_RANS_WPB 4   // one wave per SIMD: a lone wave issues its latency-bound chain ~13 % faster than two
 #endif
