@@ -5,12 +5,14 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU, in the reference bitstream format (one raster rANS stream per image).  One step =
 the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-599) for one 32-frame batch:
 compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
-rANS decode).  Every decode pass decodes exactly one 32-frame batch (32 frames in flight per pass).
+rANS decode).  Every batch is encoded as its own 32-frame wavefront pass; images are independent in the reference
+format (one rANS stream each), so the decoder groups them freely.
 
-Schedule of the headline (`value`, `--team 8`, the default): one encoder handle compresses batch after batch on its
-own HIP stream (host rANS on helper threads); every 8 encoded batches are decoded by ONE persistent k_dec_team launch
-(lbc_decode_team: one team of workgroups per 32-frame batch, team barriers instead of kernel boundaries) on a second
-stream, beside the encoder's next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
+Schedule of the headline (`value`, `--team 8 --team-batches 2`, the default): one encoder handle compresses batch
+after batch on its own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the
+remainder) are decoded by ONE persistent k_dec_team launch (lbc_decode_team: one team of workgroups per two batches,
+their 64 images side by side, team barriers instead of kernel boundaries) on a second stream, beside the encoder's
+next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
 shared weights, each compressing, entropy coding and decoding whole batches) or, with `--workers 0`, the encoder +
 `--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
 decompressions of the same batches, fill and drain included; inputs are resident in HBM when it starts.  Reported
@@ -85,6 +87,13 @@ def parse_args(argv=None):
                     help="headline schedule: one encoder handle compresses the batches while groups of TEAM encoded "
                          "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
                          "workgroups per 32-frame batch); 0 = the --workers / --depth schedules")
+    ap.add_argument("--team-batches", type=int, default=2, choices=(1, 2),
+                    help="team schedule: encoded 32-frame batches per decode team (2: each team of a launch decodes the "
+                         "64 images of two batches side by side, 4 row tiles per weight fetch; a launch then holds up "
+                         "to 2 x TEAM batches)")
+    ap.add_argument("--team-sizes", default="",
+                    help="team schedule: explicit batches per decode launch, comma-separated, summing to --steps "
+                         "(default: from --team-groups)")
     ap.add_argument("--team-groups", default="last-full", choices=("last-full", "first-full"),
                     help="when --steps is not a multiple of --team: the partial group is the first launch (last-full) "
                          "or the last one (first-full)")
@@ -381,12 +390,18 @@ def main():
                 to0 = dec_models[0].team_stats()["timeout_fallbacks"]
             errs = []
 
-            # group sizes: with --team-groups last-full (default) a partial group comes FIRST, so the launch that
-            # runs alone after the last encode (the drain) is a full one and the first launch starts earlier
-            nfull, rem = divmod(steps, team)
-            sizes = ([rem] if rem else []) + [team] * nfull
+            # group sizes (batches per launch, up to team x --team-batches): with --team-groups last-full (default) a
+            # partial group comes FIRST, so the launch that runs alone after the last encode (the drain) is a full one
+            # and the first launch starts earlier
+            tb = args.team_batches
+            nfull, rem = divmod(steps, team * tb)
+            sizes = ([rem] if rem else []) + [team * tb] * nfull
             if args.team_groups == "first-full":
                 sizes = sizes[::-1]
+            if args.team_sizes and steps == args.steps:
+                sizes = [int(v) for v in args.team_sizes.split(",")]
+                if sum(sizes) != steps or max(sizes) > team * tb or min(sizes) < 1:
+                    raise SystemExit(f"--team-sizes {args.team_sizes}: must sum to {steps}, each 1..{team * tb}")
 
             def team_decoder():
                 pend = []
@@ -402,12 +417,17 @@ def main():
                             sts = [f_.result() for (_, _, f_) in pend]
                             last = gi == len(sizes)
                             sd_ = s_decs[0]
+                            # teams of tb_ batches (their images side by side: a team of 2 x 32 images); a group of
+                            # an odd count: one batch per team
+                            tb_ = tb if len(pend) % tb == 0 else 1
+                            tsts = [[s_ for st_ in sts[i:i + tb_] for s_ in st_] for i in range(0, len(sts), tb_)]
                             with torch.cuda.stream(sd_):
                                 # (two workgroups per CU for the last launch measured slower:
                                 # profiles/r02_exp/team_two_per_cu.txt)
-                                zs = decompress_teams(dec_models[:len(pend)], sts, Hb, Wb,
+                                zt = decompress_teams(dec_models[:len(tsts)], tsts, Hb, Wb,
                                                       wg_per_cu=args.drain_wg_per_cu if last else 1)
                                 sd_.synchronize()
+                            zs = [z_[e * n:(e + 1) * n] for z_ in zt for e in range(tb_)]
                             with plock:
                                 ph["decode"] += time.perf_counter() - t0_
                             if prof:
@@ -586,6 +606,13 @@ def main():
             compress_side(scratch, frames_of(0), m_, s_)
     if args.warmup > 0:
         pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup", workers=args.workers, team=args.team)
+    if args.team and args.team_batches > 1:
+        # teams of several batches: every decoder handle's workspace sized for a team's images, before the timed region
+        # (one untimed launch of full teams on the warmup batch's streams)
+        from lbic.model import decompress_teams
+        with torch.cuda.stream(s_decs[0]):
+            decompress_teams(dec_models[:args.team], [st0 * args.team_batches] * args.team, Hb, Wb)
+            s_decs[0].synchronize()
 
     # ---- headline: the reference bitstream format, one 32-frame batch per decode pass
     dt, phase, (r, streams, z), kstats = pipeline(args.steps, depth, prof=True, label="headline", workers=args.workers,
@@ -652,6 +679,7 @@ def main():
     if args.cpu_budget > 0 and world == 1:
         cpu = cpu_baseline(arch, sd, H, W, args.cpu_budget)
 
+    tb_cfg = args.team_batches if args.team else 1
     out = {
         "metric": METRIC if (args.config, H, W) == ("B8_lowrate", 768, 768) else
         f"Mpixels/s encode+decode, {args.config} N{N}M{M}, {W}×{H}", "value": round(value, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
@@ -660,20 +688,23 @@ def main():
         "data": f"synthetic: seeded uint8 noise frames, seeded synthetic weights at the '{args.rate}' operating point "
                 "(no checkpoints / Kodak offline)",
         "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
-                               f"in the reference bitstream format (one raster rANS stream per image); each decode pass "
-                               f"decodes one {n}-frame batch ({n} frames in flight per pass), "
-                               + (f"up to {args.team} passes in flight (one team of workgroups per batch in one persistent "
-                                  "launch)" if args.team else
+                               f"in the reference bitstream format (one raster rANS stream per image); "
+                               + (f"each batch encoded as its own {n}-frame wavefront pass; decode: one persistent launch "
+                                  f"per group of up to {args.team * tb_cfg} batches, {tb_cfg} batch(es) per team of "
+                                  f"workgroups ({n * tb_cfg} images per team side by side), up to {args.team} teams per "
+                                  "launch" if args.team else
+                                  f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
                                   f"up to {args.workers} passes in flight (one per worker)" if args.workers else
+                                  f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
                                   f"{depth} pass(es) in flight beside the encoder"),
                    "batch_per_gpu": n, "frame": [H, W], "parallelism": f"images sharded over {world} GPU(s)",
-                   "global_batch": n * world, "frames_in_flight_per_decode_pass": n,
+                   "global_batch": n * world, "frames_in_flight_per_decode_pass": n * (tb_cfg if args.team else 1),
                    "decode_passes_in_flight": args.team or args.workers or depth,
                    "frames_per_encode_pass": n * (args.enc_pass if args.team else 1),
                    "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
-                                f"helper threads; every {args.team} encoded batches are decoded by ONE persistent "
+                                f"helper threads; every {args.team * tb_cfg} encoded batches are decoded by ONE persistent "
                                 "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "
-                                "32-frame batch, team barriers instead of kernel boundaries), beside the next encodes"
+                                f"{tb_cfg} batch(es), team barriers instead of kernel boundaries), beside the next encodes"
                                 if args.team else
                                 f"workers: {args.workers} codec handles on one weight set, each with its own HIP stream "
                                 "and host thread, take the batches in turn and compress, entropy code (host rANS) and "

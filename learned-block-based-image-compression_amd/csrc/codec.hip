@@ -1692,8 +1692,12 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
         if (!team_fast_path(d, S)) continue;
         a.ni_max = std::max(a.ni_max, (items + S - 1) / S);
     }
+    // rANS waves per workgroup: two once the team has more images than workgroups (each wave then keeps one image's
+    // coder state in LDS up to 2 S images; beyond that each wave decodes its rows one after another)
+    a.nrw = n_img > S ? 2 : 1;
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
-    // before it run beside the rANS decode when every workgroup takes the fast path for it
+    // before it run beside the rANS decode (on the waves the rANS decode leaves free) when every workgroup takes the
+    // fast path for it
     a.split_op = -1;
     a.split_wy = 0;
     for (int i = 0; i + 1 < (int)ops.size(); ++i) {
@@ -1709,7 +1713,8 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
         const int nkb = d.K >> 4, kby = last.k0 >> 4;
         int wy = 0;
         while (wy < KSPLIT && (wy + 1) * nkb / KSPLIT <= kby) ++wy;
-        if (wy >= 1 && wy <= KSPLIT - 1) {
+        wy = std::min(wy, KSPLIT - a.nrw);
+        if (wy >= 1) {
             a.split_op = i + 1;
             a.split_wy = wy;
         }

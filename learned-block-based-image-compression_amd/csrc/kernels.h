@@ -107,7 +107,8 @@ struct RansArgs {
 // per batch ("team", the workgroups of one blockIdx % 8 slot), team barriers between the recorded operations of a raster step instead of kernel boundaries
 constexpr int TEAM_MAX = 8;        // teams per launch
 constexpr int TEAM_MAXOPS = 24;    // operations per raster step
-constexpr int TEAM_NI_MAX = 6;     // output tiles per workgroup and GEMM on the team kernel's fast path
+constexpr int TEAM_NI_MAX = 10;    // output tiles per workgroup and GEMM on the team kernel's fast path (64 images per
+                                   // team: the context net's N = 1,152 layer deals 9 to a workgroup)
 struct TeamArgs {
     const GemmArgs* gemm;    // [T][3][NG] prepared GEMMs of one raster step, per team and column class
                              // (0: h = 0, 1: 0 < h < Wb - 1, 2: h = Wb - 1); block rows / columns set in-kernel
@@ -131,6 +132,8 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team P: 1, 2, 4 or 8 (T <= 8 / P: team t = the workgroups on slots P t ..
                              // P t + P - 1, S ranks over P XCDs; P > 1: hand-offs write-through, plain = 0)
+    int nrw;                 // rANS waves per workgroup (1 or 2: images per team up to S or 2 S decode side by side,
+                             // wave i the rows rank + i S, rank + (i + nrw) S, ...)
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {

@@ -149,7 +149,8 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
                                                 float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int LL = EXACT ? L : L + 1;
     constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
-    constexpr int NOMAX = TEAM_NI_MAX / 2;       // output elements per thread (ni * 256 over 512 threads)
+    constexpr int NPRE = 3;                      // output elements per thread (ni * 256 over 512 threads) whose epilogue
+                                                 // operands are requested before the chains: every one up to 6 tiles
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = g.K >> 4;
@@ -162,11 +163,11 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
     const int nout = ni * 256;
     dstamp(dts, 0, 0.f);
-    float bb[NOMAX], xx[NOMAX];
+    float bb[NPRE], xx[NPRE];
     if (ph != 1) {
 #pragma unroll
-        for (int q = 0; q < NOMAX; ++q) {        // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
-            const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NOMAX
+        for (int q = 0; q < NPRE; ++q) {         // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
+            const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NPRE
             const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
             const int nt = nt0 + (rank + j * S) / MT;
             const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
@@ -232,17 +233,35 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     }
     if (ph == 1) return;
     wg_bar();
+    // output o = threadIdx.x + 512 (NPRE r + q), round r: item j = o >> 8; its K slices' partials summed in slice order,
+    // then the epilogue.  Round 0's operands came before the chains; a further round (more than six tiles: 64 images
+    // per team, the context net's wide layers) loads its own into the same registers (a rolled loop: the epilogue's
+    // NPRE inlined copies serve every round)
+#pragma unroll 1
+    for (int r = 0; (int)threadIdx.x + 512 * NPRE * r < nout; ++r) {
+        if (r > 0) {
 #pragma unroll
-    for (int q = 0; q < NOMAX; ++q) {
-        const int o = threadIdx.x + 512 * q;
-        if (o >= nout) break;
-        const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
-        float vv = red[j * KSPLIT * 256 + ee];
+            for (int q = 0; q < NPRE; ++q) {
+                const int o = min((int)threadIdx.x + 512 * (NPRE * r + q), nout - 1);
+                const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
+                const int nt = nt0 + (rank + j * S) / MT;
+                const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
+                bb[q] = g.bias[ecol];
+                xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+            }
+        }
 #pragma unroll
-        for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
-        const int nt = nt0 + (rank + j * S) / MT;
-        const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
-        if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb[q], xx[q], wt);
+        for (int q = 0; q < NPRE; ++q) {
+            const int o = threadIdx.x + 512 * (NPRE * r + q);
+            if (o >= nout) break;
+            const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
+            float vv = red[j * KSPLIT * 256 + ee];
+#pragma unroll
+            for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
+            const int nt = nt0 + (rank + j * S) / MT;
+            const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
+            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb[q], xx[q], wt);
+        }
     }
     dstamp(dts, 4, 0.f);
 }
@@ -275,6 +294,32 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     }
     if (ph == 1) return;     // (the host splits a GEMM only where every workgroup takes the path above)
     team_gemm_long(g, v, h, rank, S, nt0, ntn, red, wt);
+}
+
+// the rANS decode of one wave of the team kernel: rows r0, r0 + nrw S, ... of the team's batch, in LDS area I (per
+// wave: [window RANS_WIN words][coder-state cache RC_WORDS words][centre intervals 256 words], from the LDS base).
+// Not inlined: the coder gets a register allocation of its own (inlined beside the GEMM instances, the sparse
+// kernel spilled 25-30 VGPRs to scratch, reloaded in every GEMM epilogue).  The LDS (the kernel's dynamic array,
+// declared here again: LDS instructions, not flat ones) and the recorded arguments (constant address space: scalar
+// loads) keep their address spaces across the call.
+constexpr int TEAM_RW = RANS_WIN + RC_WORDS + 256;
+typedef const __attribute__((address_space(4))) RansArgs* crans_p;
+template <bool DENSE, int I>
+__device__ __attribute__((noinline)) void team_rans(crans_p rp, int r0, int S, int nrw, int lane, bool wt, int tab_off) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
+    const RansArgs& R = *(const RansArgs*)rp;
+    uint32_t* lwin = team_lds + I * TEAM_RW;
+    uint32_t* llf = lwin + RANS_WIN + RC_WORDS;
+    if (!DENSE && r0 < R.rows && r0 + nrw * S >= R.rows) {
+        // one image per wave, the same one at every step: the coder state stays in LDS
+        rans_row_sparse<true, true>(R, lwin, r0, lane, wt, nullptr, lwin + RANS_WIN, nullptr, nullptr, nullptr, nullptr,
+                                    llf);
+    } else {
+        for (int r = r0; r < R.rows; r += nrw * S) {
+            if constexpr (DENSE) rans_row<true>(R, reinterpret_cast<uint16_t*>(team_lds + tab_off), r, lane, lwin, wt);
+            else rans_row_sparse<true>(R, lwin, r, lane, wt, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, llf);
+        }
+    }
 }
 
 // team barrier: every wave's stores drained, one arrival per workgroup, one lane polls (relaxed, s_sleep between
@@ -317,18 +362,16 @@ __device__ __forceinline__ bool team_sync(unsigned* ctr, unsigned target, unsign
 // low-rate one keeps its register allocation.
 template <bool DENSE>
 __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
-    // dynamic LDS, sized by the host (team_lds_bytes):
-    // [rANS window RANS_WIN words][rANS cache RC_WORDS words][control CTL_WORDS words][rANS centre intervals 256 words]
-    // [GEMM partials ni_max x KSPLIT x 256 floats]
-    // [dense rANS only: the table image, total16 16-bit entries]
+    // dynamic LDS, sized by the host (team_lds_bytes), per rANS wave i < nrw: [rANS window RANS_WIN words]
+    // [rANS cache RC_WORDS words][rANS centre intervals 256 words]; then [control CTL_WORDS words]
+    // [GEMM partials ni_max x KSPLIT x 256 floats][dense rANS only: the table image, total16 16-bit entries]
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
-    uint32_t* lwin = team_lds;
-    uint32_t* rcache = team_lds + RANS_WIN;                              // rans_row_sparse<.., true>'s state cache
-    uint32_t* ctl = team_lds + RANS_WIN + RC_WORDS;
+    const int nrw = ta.nrw;
+    uint32_t* ctl = team_lds + nrw * TEAM_RW;
     int& sflag = *reinterpret_cast<int*>(ctl + 18);
-    uint32_t* llf = team_lds + RANS_WIN + RC_WORDS + CTL_WORDS;          // rans_row_sparse's vector runs
-    float* red = reinterpret_cast<float*>(team_lds + RANS_WIN + RC_WORDS + CTL_WORDS + 256);
-    if (threadIdx.x == 0) rcache[4] = 0u;     // no cached coder state yet (ordered by the barriers below)
+    float* red = reinterpret_cast<float*>(ctl + CTL_WORDS);
+    if (threadIdx.x < 2 && (int)threadIdx.x < nrw)     // no cached coder state yet (ordered by the barriers below)
+        team_lds[threadIdx.x * TEAM_RW + RANS_WIN + 4] = 0u;
     const int T = ta.T, S = ta.S;
     // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
     // whatever T is); the others leave at once
@@ -346,7 +389,6 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     // the recorded operations are read-only for the launch: constant address space, so their fields come in by
     // scalar loads into SGPRs like kernel arguments (the scalar cache only reads)
     typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
-    typedef const __attribute__((address_space(4))) RansArgs* crans_p;
     const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
     const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
     unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 256 : nullptr;
@@ -388,22 +430,18 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                     team_gemm_any(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
                                   samp ? ts + 64 + op * 8 : nullptr);
                 } else {
-                    // the rANS decode on the last wave; beside it the first split_wy waves compute the K slices of
-                    // the next GEMM (the decoder's first layer) that do not read y_qnt
+                    // the rANS decode on the last nrw waves (wave i: rows rank + i S, rank + (i + nrw) S, ...); beside
+                    // it the first split_wy <= KSPLIT - nrw waves compute the K slices of the next GEMM (the decoder's
+                    // first layer) that do not read y_qnt
                     const bool sstep = tsr && v == ta.sv && h == ta.sh && rank < 32;
-                    if (wave == (ta.split_op >= 0 ? KSPLIT - 1 : 0)) {
-                        if (!DENSE && rank < R.rows && rank + S >= R.rows) {
-                            // one image per workgroup, the same one at every step: the coder state stays in LDS
-                            rans_row_sparse<true, true>(R, lwin, rank, lane, wt, nullptr, rcache, nullptr, nullptr,
-                                                        nullptr, nullptr, llf);
-                        } else {
-                            for (int r = rank; r < R.rows; r += S) {
-                                if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, wt);
-                                else rans_row_sparse<true>(R, lwin, r, lane, wt, nullptr, nullptr, nullptr, nullptr,
-                                                           nullptr, nullptr, llf);
-                            }
-                        }
-                        if (sstep && lane == 0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
+                    const int rw0 = ta.split_op >= 0 ? KSPLIT - nrw : 0;
+                    if (wave >= rw0 && wave < rw0 + nrw) {
+                        // wave i's LDS area at a compile-time offset (two call sites): a runtime base costs registers
+                        // in the coder's loop
+                        const int toff = (int)(reinterpret_cast<uint32_t*>(tab) - team_lds);
+                        if (wave == rw0) team_rans<DENSE, 0>((crans_p)(ta.rans) + team, rank, S, nrw, lane, wt, toff);
+                        else team_rans<DENSE, 1>((crans_p)(ta.rans) + team, rank + S, S, nrw, lane, wt, toff);
+                        if (sstep && lane == 0 && wave == rw0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
                         team_gemm_any(g, v, h, rank, S, red, wt, 1, ta.split_wy, nullptr);
@@ -435,7 +473,7 @@ int team_blocks_per_cu(int dense, size_t lds) {
 }
 
 size_t team_lds_bytes(const TeamArgs& a) {
-    return (size_t)(RANS_WIN + RC_WORDS + CTL_WORDS + 256) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 +
+    return (size_t)((RANS_WIN + RC_WORDS + 256) * a.nrw + CTL_WORDS) * 4 + (size_t)a.ni_max * KSPLIT * 256 * 4 +
            (size_t)(a.dense ? 1 : 0) * a.tab16 * 2;
 }
 
@@ -443,6 +481,8 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     if (a.T < 1 || a.T > TEAM_MAX || a.S < 1 || a.nops < 1 || a.nops > TEAM_MAXOPS || !a.gemm || !a.rans || !a.sync)
         return set_error(LBC_E_ARG, "bad team decoder arguments");
     if (a.ni_max < 1 || a.ni_max > TEAM_NI_MAX) return set_error(LBC_E_ARG, "bad team decoder tile count");
+    if (a.nrw < 1 || a.nrw > 2 || (a.split_op >= 0 && (a.split_wy < 1 || a.split_wy > KSPLIT - a.nrw)))
+        return set_error(LBC_E_ARG, "bad team decoder rANS wave count");
     static const bool attr = [] {
         for (int d = 0; d < 2; ++d)
             (void)hipFuncSetAttribute(team_instance(d), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

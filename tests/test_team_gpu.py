@@ -58,10 +58,13 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
 @pytest.mark.parametrize("name,T,n,shape", [
     ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
     ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)), ("b8_lowrate_2rows", 5, 48, (2, 9)),
-    ("b8_lowrate_2rows", 8, 64, (2, 5)),
+    ("b8_lowrate_2rows", 8, 64, (2, 5)), ("b8_lowrate_2rows", 3, 50, (2, 6)), ("b8_lowrate_2rows", 2, 96, (2, 4)),
 ])
 def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
-    """Image counts of one, two, three and four row tiles, 1-8 teams."""
+    """Image counts of one to six row tiles, 1-8 teams.  64 images on a team of 32 workgroups (the bench's two-batch
+    teams): up to 9 output tiles per workgroup on the fast path and two rANS waves per workgroup, each keeping its
+    image's coder state in LDS; 50: some workgroups with one image; 96: three images per workgroup (each rANS wave
+    decodes its rows one after another) and six row tiles (the long GEMM path)."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")     # the team kernel decodes with the sparse rANS variant
     g = load_golden("loop_" + name)
     Hb, Wb = shape or g["x"].shape[:2]
@@ -112,7 +115,7 @@ def test_team_two_workgroups_per_cu(name, T, n, shape, monkeypatch):
 
 @pytest.mark.parametrize("spread", [1, 2])
 @pytest.mark.parametrize("name,T,n,shape", [("b8_lowrate_2rows", 4, 32, (2, 24)), ("tiny_ks3311", 3, 5, (3, 4)),
-                                            ("b8_lowrate_2rows", 1, 35, (2, 7))])
+                                            ("b8_lowrate_2rows", 1, 35, (2, 7)), ("b8_lowrate_2rows", 2, 64, (2, 6))])
 def test_team_spread_two_xcds(name, T, n, shape, spread, monkeypatch):
     """At most four batches: by default each team takes the workgroups of two XCD slots (twice the ranks,
     write-through hand-offs); LBIC_TEAM_SPREAD=1 keeps one XCD per team (plain hand-offs) -- the same results as the
@@ -141,7 +144,8 @@ def test_team_small_teams(S, monkeypatch):
 
 @pytest.mark.parametrize("name,T,n,shape,scale", [
     ("tiny_ks3111", 3, 5, None, 0.05), ("tiny_ks3311", 8, 3, None, 0.05), ("b8_lowrate_2rows", 4, 32, (2, 24), 0.05),
-    ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0)])
+    ("b8_lowrate_2rows", 2, 35, (2, 7), 4.0), ("tiny_ks3311", 3, 4, (3, 5), 4.0),
+    ("b8_lowrate_2rows", 2, 64, (2, 7), 0.05)])
 def test_team_dense_rans(name, T, n, shape, scale, monkeypatch):
     """The dense rANS variant inside the team kernel (high rates; every workgroup stages the tables in its LDS once per
     launch, one wave per stream runs rans_row<true>): forced by LBIC_RANS_SPARSE=0 at the fixtures' low rates, and
