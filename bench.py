@@ -348,7 +348,7 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0)
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, windows=[], enc_done=0.0)
 
     def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
@@ -385,7 +385,7 @@ def main():
             dq = queue.Queue(maxsize=2 * team)
             if prof:
                 for kk in team_acc:
-                    team_acc[kk] = [] if kk == "plain" else 0
+                    team_acc[kk] = [] if kk in ("plain", "windows") else 0
                 team_acc["hw"] = Hb * Wb
                 to0 = dec_models[0].team_stats()["timeout_fallbacks"]
             errs = []
@@ -439,6 +439,8 @@ def main():
                                 team_acc["steps"] += len(pend) * Hb * Wb
                                 team_acc["plain"].append(st_["plain"])
                                 team_acc["timeouts"] = st_["timeout_fallbacks"] - to0
+                                team_acc["windows"].append([round(t0_ - t0, 3), round(time.perf_counter() - t0, 3),
+                                                            len(pend), len(tsts)])
                             for (k_, r_, _), st_, z_ in zip(pend, sts, zs):
                                 finish(k_, r_, st_, z_)
                             pend = []
@@ -471,6 +473,8 @@ def main():
                         dq.put((base + k + e, r_ if k + e == steps - 1 else None, f_))
                     del rs_, r_
                     k += g
+                if prof:
+                    team_acc["enc_done"] = round(time.perf_counter() - t0, 3)
                 dq.put(None)
                 dth.join()
             if errs:
@@ -808,6 +812,7 @@ def roofline(kstats, dt, team=None, enc=None, steps=0):
                                      wall_occupancy_s=round(team["ms"] / 1e3, 4),
                                      plain_handoffs=team["plain"],
                                      barrier_timeout_fallbacks=team["timeouts"],
+                                     launch_windows_s=team["windows"], encoder_done_s=team["enc_done"],
                                      batches_per_launch=round(team["steps"] / team["launches"] / team["hw"], 3),
                                      batch_decode_latency_ms=round(per, 3),
                                      launch_ms_per_batch=round(team["ms"] * team["hw"] / team["steps"], 3),
@@ -834,8 +839,9 @@ def roofline(kstats, dt, team=None, enc=None, steps=0):
 
     def traffic_of(name):
         pm = traffic_db.get(name, {})
-        if name == "k_dec_team" and team and "hbm_bytes_per_team_step" in pm:
-            return round(pm["hbm_bytes_per_team_step"] * team["steps"] / team["launches"]), pm.get("source")
+        if name == "k_dec_team" and team and "hbm_bytes_per_batch_step" in pm:
+            # (counters at the headline's team shape; team["steps"] counts 32-frame batch raster steps)
+            return round(pm["hbm_bytes_per_batch_step"] * team["steps"] / team["launches"]), pm.get("source")
         if "hbm_bytes_per_dispatch" in pm:
             return round(pm["hbm_bytes_per_dispatch"]), pm.get("source")
         return None, None

@@ -123,7 +123,7 @@ def test_bench_roofline_dominance_is_wall_occupancy():
                                total_flops=5e11, total_bytes=5e10)}
     enc = dict(ms=3500.0, passes=20)
     team = dict(launches=3, ms=3900.0, bytes=3 * 1.9e12, flops=3 * 2.8e13, steps=20 * 9216, plain=[1, 1, 1],
-                timeouts=0, hw=9216)
+                timeouts=0, hw=9216, windows=[[0.4, 1.7, 4, 4], [1.8, 3.1, 8, 8], [3.2, 4.5, 8, 8]], enc_done=3.1)
     roof, kernels = bench.roofline(kstats, dt, team, enc, steps)
     assert roof["kernel"] == "k_dec_team", roof
     assert roof["wall_occupancy_ms_per_step"] <= dt / steps * 1e3      # the dominant kernel fits in the step
