@@ -91,6 +91,8 @@ def parse_args(argv=None):
                     help="team schedule: encoded 32-frame batches per decode team (2: each team of a launch decodes the "
                          "64 images of two batches side by side, 4 row tiles per weight fetch; a launch then holds up "
                          "to 2 x TEAM batches)")
+    ap.add_argument("--first-team-batches", type=int, default=0, choices=(0, 1, 2),
+                    help="team schedule: batches per team in the FIRST decode launch (0: --team-batches)")
     ap.add_argument("--team-sizes", default="",
                     help="team schedule: explicit batches per decode launch, comma-separated, summing to --steps "
                          "(default: from --team-groups)")
@@ -350,7 +352,7 @@ def main():
 
     team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, windows=[], enc_done=0.0)
 
-    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0):
+    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0, tbatches=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
         (or `gang` batches in one wavefront pass) while a helper thread entropy codes the previous one and
         `depth` decoder threads each decode `gang` queued batches per raster pass (their own handles and
@@ -393,7 +395,7 @@ def main():
             # group sizes (batches per launch, up to team x --team-batches): with --team-groups last-full (default) a
             # partial group comes FIRST, so the launch that runs alone after the last encode (the drain) is a full one
             # and the first launch starts earlier
-            tb = args.team_batches
+            tb = tbatches or args.team_batches
             nfull, rem = divmod(steps, team * tb)
             sizes = ([rem] if rem else []) + [team * tb] * nfull
             if args.team_groups == "first-full":
@@ -419,7 +421,8 @@ def main():
                             sd_ = s_decs[0]
                             # teams of tb_ batches (their images side by side: a team of 2 x 32 images); a group of
                             # an odd count: one batch per team
-                            tb_ = tb if len(pend) % tb == 0 else 1
+                            tb_ = args.first_team_batches if gi == 1 and args.first_team_batches and not tbatches else tb
+                            tb_ = tb_ if len(pend) % tb_ == 0 else 1
                             tsts = [[s_ for st_ in sts[i:i + tb_] for s_ in st_] for i in range(0, len(sts), tb_)]
                             with torch.cuda.stream(sd_):
                                 # (two workgroups per CU for the last launch measured slower:
@@ -623,6 +626,11 @@ def main():
                                                   team=args.team)
 
     side = {}
+    if args.side_steps > 0 and args.team and args.team_batches > 1:
+        # the same schedule with one 32-frame batch per decode team (the round-4 geometry), same number of batches
+        d_, p_, _, _ = pipeline(args.steps, depth, label="one batch per team", team=args.team, tbatches=1)
+        side["one_batch_per_team"] = summary(d_, p_, args.steps, frames_in_flight_per_decode_pass=n,
+                                             decode_passes_in_flight=args.team)
     if args.side_steps > 0 and (depth != 1 or args.team or args.workers):
         d_, p_, _, _ = pipeline(args.side_steps, 1, label="one decode in flight")
         side["one_decode_in_flight"] = summary(d_, p_, args.side_steps, frames_in_flight_per_decode_pass=n,

@@ -13,7 +13,7 @@ import sys
 
 def main():
     out, encf, teamf = sys.argv[1:4]
-    T, Hb, Wb, n = (int(x) for x in (sys.argv[4:8] if len(sys.argv) > 7 else (8, 96, 96, 32)))
+    T, Hb, Wb, nimg = (int(x) for x in (sys.argv[4:8] if len(sys.argv) > 7 else (8, 96, 96, 32)))
     enc, team = json.load(open(encf)), json.load(open(teamf))
     res = {}
     z = {"dispatches": 0, "hbm_bytes_per_dispatch": 0.0}
@@ -31,11 +31,11 @@ def main():
                                 source="every dispatch of the encoder graph, dispatch-weighted")
     t = dict(team["k_dec_team"])
     t["hbm_bytes_per_team_step"] = t["hbm_bytes_per_dispatch"] / (T * Hb * Wb)
-    t["hbm_bytes_per_batch_step"] = t["hbm_bytes_per_dispatch"] / (T * n / 32 * Hb * Wb)
-    t["images_per_team"] = n
+    t["hbm_bytes_per_batch_step"] = t["hbm_bytes_per_dispatch"] / (T * nimg / 32 * Hb * Wb)
+    t["images_per_team"] = nimg
     if "TCC_HIT_sum" in t:
         t["l2_hit_rate"] = t["TCC_HIT_sum"] / (t["TCC_HIT_sum"] + t["TCC_MISS_sum"])
-    t["source"] = f"tools/team_exp.py under PMC passes: {T} teams of {n} images x {Hb}x{Wb} blocks per dispatch"
+    t["source"] = f"tools/team_exp.py under PMC passes: {T} teams of {nimg} images x {Hb}x{Wb} blocks per dispatch"
     res["k_dec_team"] = t
     res["_source"] = {"note": "FETCH_SIZE x 2 + WRITE_SIZE, x 1024 bytes (MI355X_MICROARCH.md HBM section)"}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
