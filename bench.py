@@ -350,7 +350,8 @@ def main():
                     acc[k_] += st_[k_]
         return ks
 
-    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, windows=[], enc_done=0.0)
+    team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, windows=[], enc_done=0.0,
+                    modes=[])
 
     def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0, tbatches=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
@@ -387,7 +388,7 @@ def main():
             dq = queue.Queue(maxsize=2 * team)
             if prof:
                 for kk in team_acc:
-                    team_acc[kk] = [] if kk in ("plain", "windows") else 0
+                    team_acc[kk] = [] if kk in ("plain", "windows", "modes") else 0
                 team_acc["hw"] = Hb * Wb
                 to0 = dec_models[0].team_stats()["timeout_fallbacks"]
             errs = []
@@ -441,6 +442,7 @@ def main():
                                 team_acc["flops"] += st_["flops"]
                                 team_acc["steps"] += len(pend) * Hb * Wb
                                 team_acc["plain"].append(st_["plain"])
+                                team_acc["modes"].append(st_["mode"])
                                 team_acc["timeouts"] = st_["timeout_fallbacks"] - to0
                                 team_acc["windows"].append([round(t0_ - t0, 3), round(time.perf_counter() - t0, 3),
                                                             len(pend), len(tsts)])
@@ -821,6 +823,7 @@ def roofline(kstats, dt, team=None, enc=None, steps=0):
                                      plain_handoffs=team["plain"],
                                      barrier_timeout_fallbacks=team["timeouts"],
                                      launch_windows_s=team["windows"], encoder_done_s=team["enc_done"],
+                                     modes=team.get("modes", []),
                                      batches_per_launch=round(team["steps"] / team["launches"] / team["hw"], 3),
                                      batch_decode_latency_ms=round(per, 3),
                                      launch_ms_per_batch=round(team["ms"] * team["hw"] / team["steps"], 3),

@@ -347,6 +347,20 @@ int pack_gdn(lbc_model* m, Layer& L, const std::string& name, int C) {
     return upload_layer(L, wkn, beta, pad16(C), C);
 }
 
+// zero a fresh workspace buffer on the handle's non-blocking stream and wait for it: a hipMemset on the legacy stream
+// fails while another thread of the process captures a graph (a decoder handle sizing its workspace beside another
+// handle's first row-graph capture, bench.py's sub-stream leg)
+static int ws_zero(lbc_model* m, void* p, size_t b) {
+    hipStream_t z = m->cap2;
+    if (!z) {
+        HIPCHK(hipMemset(p, 0, b));
+        return LBC_OK;
+    }
+    HIPCHK(hipMemsetAsync(p, 0, b, z));
+    HIPCHK(hipStreamSynchronize(z));
+    return LBC_OK;
+}
+
 int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
     if (m->ws_n == n_img && m->ws_Hb == Hb && m->ws_Wb == Wb) return LBC_OK;
     const int T = (Wb - 1) + 2 * (Hb - 1) + 1;
@@ -406,7 +420,7 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
         if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4)))) return rc;
         const size_t b = (size_t)n_img * (Hb + 2) * (Wb + 4) * m->C1P * sizeof(float);
         if ((rc = m->l0.alloc(b))) return rc;
-        HIPCHK(hipMemset(m->l0.p, 0, b));    // pad channels stay 0 (never written; A x 0-weight must not meet NaN)
+        if ((rc = ws_zero(m, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
     }
     const size_t F = sizeof(float);
     if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
@@ -423,7 +437,7 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
         for (int i = 0; i < 10; ++i) {
             if (l > 0 && (i == 4 || i == 5)) continue;   // encoder-only buffers
             if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
-            HIPCHK(hipMemset(bufs[i]->p, 0, rows * widths[i] * F));
+            if ((rc = ws_zero(m, bufs[i]->p, rows * widths[i] * F))) return rc;
         }
     }
     m->Mmax = mmax;
@@ -1763,7 +1777,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         ms[0]->team_plain_last = -1;    // no team launch: lbc_team_stats reports the decode's own events (ev[2..3])
         return LBC_OK;
     }
-    const int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
+    int sparse = rans_sparse_choice(lens, T * n_img, (double)T * n_img * Hb * Wb * ms[0]->M);
     const double zbytes = (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->Cx * 4;
     const double lbytes = ms[0]->l0_on ? (double)n_img * (Hb + 2) * (Wb + 4) * ms[0]->C1P * 4 : 0.0;
     if ((te && atoi(te) == 0) || ms[0]->M > 256 || zbytes >= 4294967296.0 || lbytes >= 4294967296.0)
@@ -1810,7 +1824,16 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory
         a.dense = sparse ? 0 : 1;
-        const size_t lds = team_lds_bytes(a);
+        size_t lds = team_lds_bytes(a);
+        if (lds > 160 * 1024 && a.dense) {
+            // the dense tables do not fit beside this geometry's partials (high rates with many tiles per workgroup):
+            // the sparse coder -- tables read from global memory, any rate, bit-identical -- instead of the row graphs
+            sparse = 1;
+            if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse))) return rc;
+            a = m0->team_args;
+            a.dense = 0;
+            lds = team_lds_bytes(a);
+        }
         if (lds > 160 * 1024) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
         const int nb = team_blocks_per_cu(a.dense, lds);
         if (nb >= wpc) break;

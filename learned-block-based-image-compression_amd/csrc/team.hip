@@ -299,25 +299,33 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
 // the rANS decode of one wave of the team kernel: rows r0, r0 + nrw S, ... of the team's batch, in LDS area I (per
 // wave: [window RANS_WIN words][coder-state cache RC_WORDS words][centre intervals 256 words], from the LDS base).
 // Not inlined: the coder gets a register allocation of its own (inlined beside the GEMM instances, the sparse
-// kernel spilled 25-30 VGPRs to scratch, reloaded in every GEMM epilogue).  The LDS (the kernel's dynamic array,
-// declared here again: LDS instructions, not flat ones) and the recorded arguments (constant address space: scalar
-// loads) keep their address spaces across the call.
+// kernel spilled 25-30 VGPRs to scratch, reloaded in every GEMM epilogue).  A call's arguments travel in VGPRs: each
+// is made uniform again (readfirstlane) so the recorded RansArgs come in by scalar loads from the constant address
+// space; the LDS is the kernel's dynamic array, declared here again (LDS instructions, not flat ones).
 constexpr int TEAM_RW = RANS_WIN + RC_WORDS + 256;
 typedef const __attribute__((address_space(4))) RansArgs* crans_p;
 template <bool DENSE, int I>
-__device__ __attribute__((noinline)) void team_rans(crans_p rp, int r0, int S, int nrw, int lane, bool wt, int tab_off) {
+__device__ __attribute__((noinline)) void team_rans(unsigned long long rp, int r0, int S, int nrw, int wt, int tab_off) {
     extern __shared__ __attribute__((aligned(16))) uint32_t team_lds[];
-    const RansArgs& R = *(const RansArgs*)rp;
+    const unsigned rlo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)rp);
+    const unsigned rhi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(rp >> 32));
+    const RansArgs& R = *(const RansArgs*)(crans_p)(((unsigned long long)rhi << 32) | rlo);
+    r0 = __builtin_amdgcn_readfirstlane(r0);
+    S = __builtin_amdgcn_readfirstlane(S);
+    nrw = __builtin_amdgcn_readfirstlane(nrw);
+    const bool w = __builtin_amdgcn_readfirstlane(wt) != 0;
+    const int lane = threadIdx.x & 63;
     uint32_t* lwin = team_lds + I * TEAM_RW;
     uint32_t* llf = lwin + RANS_WIN + RC_WORDS;
     if (!DENSE && r0 < R.rows && r0 + nrw * S >= R.rows) {
         // one image per wave, the same one at every step: the coder state stays in LDS
-        rans_row_sparse<true, true>(R, lwin, r0, lane, wt, nullptr, lwin + RANS_WIN, nullptr, nullptr, nullptr, nullptr,
+        rans_row_sparse<true, true>(R, lwin, r0, lane, w, nullptr, lwin + RANS_WIN, nullptr, nullptr, nullptr, nullptr,
                                     llf);
     } else {
+        uint16_t* tab = reinterpret_cast<uint16_t*>(team_lds + __builtin_amdgcn_readfirstlane(tab_off));
         for (int r = r0; r < R.rows; r += nrw * S) {
-            if constexpr (DENSE) rans_row<true>(R, reinterpret_cast<uint16_t*>(team_lds + tab_off), r, lane, lwin, wt);
-            else rans_row_sparse<true>(R, lwin, r, lane, wt, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, llf);
+            if constexpr (DENSE) rans_row<true>(R, tab, r, lane, lwin, w);
+            else rans_row_sparse<true>(R, lwin, r, lane, w, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, llf);
         }
     }
 }
@@ -438,9 +446,10 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                     if (wave >= rw0 && wave < rw0 + nrw) {
                         // wave i's LDS area at a compile-time offset (two call sites): a runtime base costs registers
                         // in the coder's loop
+                        const unsigned long long rp = (unsigned long long)((crans_p)(ta.rans) + team);
                         const int toff = (int)(reinterpret_cast<uint32_t*>(tab) - team_lds);
-                        if (wave == rw0) team_rans<DENSE, 0>((crans_p)(ta.rans) + team, rank, S, nrw, lane, wt, toff);
-                        else team_rans<DENSE, 1>((crans_p)(ta.rans) + team, rank + S, S, nrw, lane, wt, toff);
+                        if (wave == rw0) team_rans<DENSE, 0>(rp, rank, S, nrw, wt ? 1 : 0, toff);
+                        else team_rans<DENSE, 1>(rp, rank + S, S, nrw, wt ? 1 : 0, toff);
                         if (sstep && lane == 0 && wave == rw0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);

@@ -166,6 +166,19 @@ def test_team_dense_rans(name, T, n, shape, scale, monkeypatch):
     assert hs[0].team_stats()["mode"] == "team_dense"
 
 
+def test_team_sparse_coder_at_high_rate(monkeypatch):
+    """The sparse coder (tables in global memory) at more than one bit per symbol with two rANS waves per workgroup
+    (64 images on a team of 32): what lbc_decode_team runs when the dense tables do not fit the workgroup's LDS beside
+    the geometry's partials -- bit-identical to the graph decoder."""
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    ref, got, hs, st = run_case("b8_lowrate_2rows", 2, 64, 2, 5, seed=3, scale=4.0)
+    nsym = 2 * 64 * 2 * 5 * 96
+    assert 8.0 * sum(len(s) for b in st for s in b) / nsym >= 1.0
+    for t in range(2):
+        assert torch.equal(got[t], ref[t]), f"team {t}: {(got[t] != ref[t]).sum().item()} values differ"
+    assert hs[0].team_stats()["mode"] == "team_sparse"
+
+
 def test_team_fallback_and_errors(monkeypatch):
     """LBIC_TEAM=0: the batches decode through lbc_decode one after another with the same results; a truncated stream
     raises; the handles work afterwards."""
