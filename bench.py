@@ -5,14 +5,13 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU, in the reference bitstream format (one raster rANS stream per image).  One step =
 the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-599) for one 32-frame batch:
 compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
-rANS decode).  Every batch is encoded as its own 32-frame wavefront pass; images are independent in the reference
-format (one rANS stream each), so the decoder groups them freely.
+rANS decode).  Every batch is encoded as its own 32-frame wavefront pass and decoded as its own 32-frame raster pass
+(one team of workgroups per batch).
 
-Schedule of the headline (`value`, `--team 8 --team-batches 2`, the default): one encoder handle compresses batch
-after batch on its own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the
-remainder) are decoded by ONE persistent k_dec_team launch (lbc_decode_team: one team of workgroups per two batches,
-their 64 images side by side, team barriers instead of kernel boundaries) on a second stream, beside the encoder's
-next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
+Schedule of the headline (`value`, `--team 16`, the default): one encoder handle compresses batch after batch on its
+own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the remainder) are decoded
+by ONE persistent k_dec_team launch (lbc_decode_team: one team of workgroups per 32-frame batch, two teams per XCD,
+team barriers instead of kernel boundaries) on a second stream, beside the encoder's next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
 shared weights, each compressing, entropy coding and decoding whole batches) or, with `--workers 0`, the encoder +
 `--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
 decompressions of the same batches, fill and drain included; inputs are resident in HBM when it starts.  Reported
@@ -83,11 +82,12 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=3, help="decode passes in flight beside the encoder (0 = serial)")
     ap.add_argument("--share-weights", type=int, default=1,
                     help="1: decoder handles share the encoder handle's device weights (lbc_create_sibling)")
-    ap.add_argument("--team", type=int, default=8,
+    ap.add_argument("--team", type=int, default=16,
                     help="headline schedule: one encoder handle compresses the batches while groups of TEAM encoded "
                          "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
-                         "workgroups per 32-frame batch); 0 = the --workers / --depth schedules")
-    ap.add_argument("--team-batches", type=int, default=2, choices=(1, 2),
+                         "workgroups per 32-frame batch; more than 8: two teams per XCD); 0 = the --workers / --depth "
+                         "schedules")
+    ap.add_argument("--team-batches", type=int, default=1, choices=(1, 2),
                     help="team schedule: encoded 32-frame batches per decode team (2: each team of a launch decodes the "
                          "64 images of two batches side by side, 4 row tiles per weight fetch; a launch then holds up "
                          "to 2 x TEAM batches)")
@@ -615,9 +615,9 @@ def main():
             compress_side(scratch, frames_of(0), m_, s_)
     if args.warmup > 0:
         pipeline(args.warmup, max(depth, 1) if depth else 0, label="warmup", workers=args.workers, team=args.team)
-    if args.team and args.team_batches > 1:
-        # teams of several batches: every decoder handle's workspace sized for a team's images, before the timed region
-        # (one untimed launch of full teams on the warmup batch's streams)
+    if args.team and (args.team_batches > 1 or args.team > args.warmup):
+        # every decoder handle's workspace sized for a team's images and the full launch's team program recorded before
+        # the timed region (one untimed launch of full teams on the warmup batch's streams)
         from lbic.model import decompress_teams
         with torch.cuda.stream(s_decs[0]):
             decompress_teams(dec_models[:args.team], [st0 * args.team_batches] * args.team, Hb, Wb)
@@ -628,11 +628,11 @@ def main():
                                                   team=args.team)
 
     side = {}
-    if args.side_steps > 0 and args.team and args.team_batches > 1:
-        # the same schedule with one 32-frame batch per decode team (the round-4 geometry), same number of batches
-        d_, p_, _, _ = pipeline(args.steps, depth, label="one batch per team", team=args.team, tbatches=1)
-        side["one_batch_per_team"] = summary(d_, p_, args.steps, frames_in_flight_per_decode_pass=n,
-                                             decode_passes_in_flight=args.team)
+    if args.side_steps > 0 and args.team == 16 and args.team_batches == 1:
+        # the round-4 geometry beside it: 8 teams per launch, one per XCD (each a whole XCD's CUs), same batches
+        d_, p_, _, _ = pipeline(args.steps, depth, label="8 teams per launch", team=8)
+        side["eight_teams_per_launch"] = summary(d_, p_, args.steps, frames_in_flight_per_decode_pass=n,
+                                                 decode_passes_in_flight=8)
     if args.side_steps > 0 and (depth != 1 or args.team or args.workers):
         d_, p_, _, _ = pipeline(args.side_steps, 1, label="one decode in flight")
         side["one_decode_in_flight"] = summary(d_, p_, args.side_steps, frames_in_flight_per_decode_pass=n,
@@ -706,7 +706,7 @@ def main():
                                + (f"each batch encoded as its own {n}-frame wavefront pass; decode: one persistent launch "
                                   f"per group of up to {args.team * tb_cfg} batches, {tb_cfg} batch(es) per team of "
                                   f"workgroups ({n * tb_cfg} images per team side by side), up to {args.team} teams per "
-                                  "launch" if args.team else
+                                  "launch (one per XCD up to 8, two per XCD beyond)" if args.team else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
                                   f"up to {args.workers} passes in flight (one per worker)" if args.workers else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "

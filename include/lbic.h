@@ -161,8 +161,10 @@ int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int
  * handle ms[t] (distinct handles of one geometry, e.g. lbc_create_sibling) from streams[t * n_img + i] /
  * lens[t * n_img + i] into zhat_devs[t]; results are bit-identical to lbc_decode of each batch.  All batches run
  * in ONE persistent GPU launch (k_dec_team: one team of workgroups per batch, team barriers between the operations
- * of a raster step).  The rANS operation picks its variant by rate as lbc_decode does: below 1 bit per symbol the
- * sparse one, otherwise the dense one on a copy of the tables every workgroup stages in its LDS at launch start.
+ * of a raster step; n_teams 1..16: up to 8 teams one per XCD, 9-16 two per XCD).  The rANS operation picks its variant
+ * by rate as lbc_decode does: below 1 bit per symbol the sparse one, otherwise the dense one on a copy of the tables
+ * every workgroup stages in its LDS at launch start (the sparse one where those tables do not fit beside the
+ * geometry's partials).
  * Batches the team kernel does not cover (M > 256, buffers past 4 GB) are decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
 int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *streams, const size_t *lens, int n_img,
                     int Hb, int Wb, float *const *zhat_devs, void *stream);

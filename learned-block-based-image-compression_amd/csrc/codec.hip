@@ -1695,6 +1695,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     a.T = T;
     a.S = S;
     a.spread = spread;
+    a.sub = T > TEAM_SLOTS ? 2 : 1;
     a.Hb = Hb;
     a.Wb = Wb;
     a.sync = m0->team_sync.as<unsigned>();
@@ -1751,7 +1752,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
 int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* streams, const size_t* lens, int n_img,
                     int Hb, int Wb, float* const* zhat_devs, void* stream) {
     if (!ms || !streams || !lens || !zhat_devs) return set_error(LBC_E_ARG, "null argument");
-    if (n_teams < 1 || n_teams > TEAM_MAX) return set_error(LBC_E_ARG, "1 to 8 batches per team decode");
+    if (n_teams < 1 || n_teams > TEAM_MAX) return set_error(LBC_E_ARG, "1 to 16 image sets per team decode");
     if (n_img <= 0 || Hb <= 0 || Wb <= 0) return set_error(LBC_E_ARG, "empty frame");
     const int T = n_teams;
     for (int t = 0; t < T; ++t) {
@@ -1803,19 +1804,21 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     // and the dynamic LDS of the launch, and a geometry that does not fit is shrunk (two workgroups per CU -> one) or
     // decoded by lbc_decode per batch.
     int wpc = std::max(1, m0->team_wpc);
-    int S = 0, spread = 1;
+    int S = 0, spread = 1, sub = 1;
     TeamArgs a{};
     for (;;) {
-        S = std::min(32, cus / TEAM_MAX) * wpc;
+        // more than 8 teams: two per XCD slot, each half the slot's CUs
+        sub = T > TEAM_SLOTS ? 2 : 1;
+        S = std::min(32, cus / TEAM_SLOTS) / sub * wpc;
         if (m0->team_size > 0) S = std::min(S, m0->team_size * wpc);
         // at most four batches: each team takes two XCDs (twice the workgroups, write-through hand-offs; 4 batches
         // alone: 0.917 vs 0.969 s per launch, profiles/r02_exp/team_spread.txt); LBIC_TEAM_SPREAD=P (1, 2, 4, 8 with
         // T <= 8 / P) sets the XCD slots per team (A/B runs)
         const char* spe = getenv("LBIC_TEAM_SPREAD");
-        spread = T <= TEAM_MAX / 2 ? 2 : 1;
+        spread = T <= TEAM_SLOTS / 2 ? 2 : 1;
         if (spe) {
             const int p = atoi(spe);
-            if ((p == 1 || p == 2 || p == 4 || p == 8) && T <= TEAM_MAX / p) spread = p;
+            if ((p == 1 || p == 2 || p == 4 || p == 8) && T <= TEAM_SLOTS / p) spread = p;
         }
         S *= spread;
         if (S < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);

@@ -105,7 +105,8 @@ struct RansArgs {
 
 // Team decoder (k_dec_team, team.hip): the raster decodes of T <= 8 batches in ONE persistent launch, S workgroups
 // per batch ("team", the workgroups of one blockIdx % 8 slot), team barriers between the recorded operations of a raster step instead of kernel boundaries
-constexpr int TEAM_MAX = 8;        // teams per launch
+constexpr int TEAM_SLOTS = 8;      // XCD slots of a launch (blockIdx % 8: one XCD each under round-robin placement)
+constexpr int TEAM_MAX = 16;       // teams per launch: up to two per slot (TeamArgs::sub)
 constexpr int TEAM_MAXOPS = 24;    // operations per raster step
 constexpr int TEAM_NI_MAX = 10;    // output tiles per workgroup and GEMM on the team kernel's fast path (64 images per
                                    // team: the context net's N = 1,152 layer deals 9 to a workgroup)
@@ -132,6 +133,8 @@ struct TeamArgs {
     int tab16;               // entries of the table image (RansArgs::total16; the dense variant's LDS)
     int spread;              // XCD slots per team P: 1, 2, 4 or 8 (T <= 8 / P: team t = the workgroups on slots P t ..
                              // P t + P - 1, S ranks over P XCDs; P > 1: hand-offs write-through, plain = 0)
+    int sub;                 // teams per XCD slot (1, or 2 when T > 8: team slot + 8 q = the slot's workgroups
+                             // q S .. q S + S - 1 in launch order; spread = 1)
     int nrw;                 // rANS waves per workgroup (1 or 2: images per team up to S or 2 S decode side by side,
                              // wave i the rows rank + i S, rank + (i + nrw) S, ...)
 };

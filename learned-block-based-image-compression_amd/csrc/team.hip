@@ -381,13 +381,15 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     if (threadIdx.x < 2 && (int)threadIdx.x < nrw)     // no cached coder state yet (ordered by the barriers below)
         team_lds[threadIdx.x * TEAM_RW + RANS_WIN + 4] = 0u;
     const int T = ta.T, S = ta.S;
-    // grid = 8 x S: team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin placement,
-    // whatever T is); the others leave at once
+    // grid = 8 x S (x sub): team t = the workgroups with blockIdx % 8 == t (t < T; one XCD each under round-robin
+    // placement, whatever T is); the others leave at once
     // spread P = 2, 4, 8 (at most 8 / P teams): team t = the workgroups of slots P t .. P t + P - 1 (P XCDs), ranks
     // interleaved over them
+    // sub = 2 (more than 8 teams): two teams per slot, team slot + 8 q = the slot's workgroups q S .. q S + S - 1
     const int slot = blockIdx.x & 7;
-    const int team = slot / ta.spread;
-    const int rank = (int)(blockIdx.x >> 3) * ta.spread + slot % ta.spread;
+    const int kk = (int)(blockIdx.x >> 3);
+    const int team = ta.sub > 1 ? slot + TEAM_SLOTS * (kk / S) : slot / ta.spread;
+    const int rank = ta.sub > 1 ? kk % S : kk * ta.spread + slot % ta.spread;
     if (team >= T || rank >= S) return;
     unsigned* ctr = ta.sync + team * 32;
     unsigned* fail = ta.sync + T * 32;
@@ -501,9 +503,11 @@ int launch_dec_team(const TeamArgs& a, hipStream_t s) {
     const size_t lds = team_lds_bytes(a);
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "team decoder: LDS image too large");
     if ((a.spread != 1 && a.spread != 2 && a.spread != 4 && a.spread != 8) ||
-        (a.spread > 1 && (a.T > TEAM_MAX / a.spread || a.S % a.spread || a.plain)))
+        (a.spread > 1 && (a.T > TEAM_SLOTS / a.spread || a.S % a.spread || a.plain)))
         return set_error(LBC_E_ARG, "bad team spread");
-    const dim3 grid(8 * a.S / a.spread);
+    if ((a.sub != 1 && a.sub != 2) || (a.sub == 2 && a.spread != 1) || a.T > TEAM_SLOTS * a.sub)
+        return set_error(LBC_E_ARG, "bad team count per XCD slot");
+    const dim3 grid(TEAM_SLOTS * a.S * a.sub / a.spread);
     if (a.dense) hipLaunchKernelGGL((k_dec_team<true>), grid, dim3(512), lds, s, a);
     else hipLaunchKernelGGL((k_dec_team<false>), grid, dim3(512), lds, s, a);
     return launch_status("k_dec_team");

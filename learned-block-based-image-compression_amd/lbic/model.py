@@ -418,15 +418,16 @@ class BlockBasedImgCompLossyNetv9:
 
 def decompress_teams(models: Sequence["BlockBasedImgCompLossyNetv9"], batches: Sequence[Sequence[bytes]], Hb: int, Wb: int,
                      wg_per_cu: int = 1, team_size: int = 0):
-    """Decode len(batches) <= 8 batches of reference-format bitstreams in ONE persistent launch (lbc_decode_team):
+    """Decode len(batches) <= 16 batches of reference-format bitstreams in ONE persistent launch (lbc_decode_team: one
+    team of workgroups per batch on one XCD; more than 8 batches: two teams per XCD, each half its CUs):
     batch t by models[t] (distinct handles of one geometry, e.g. siblings), each batch the same number of images of
     Hb x Wb blocks.  Returns [zhat_t [n, Hb, Wb, 3B^2]], bit-identical to models[t].decompress_batch(batches[t]).
     wg_per_cu (LBC_OPT_TEAM_WG_PER_CU): 1 leaves room for an encoder running beside the launch; 2 doubles each
     team's workgroups (every register of the GPU) for a decode with the GPU otherwise idle.  team_size
     (LBC_OPT_TEAM_SIZE): workgroups per team, 0 = one per CU of an XCD; fewer: small teams."""
     T = len(batches)
-    if T < 1 or T > 8 or len(models) < T:
-        raise ValueError("1 to 8 batches, one model handle each")
+    if T < 1 or T > 16 or len(models) < T:
+        raise ValueError("1 to 16 batches, one model handle each")
     n = len(batches[0])
     if any(len(b) != n for b in batches):
         raise ValueError("every batch needs the same number of images")

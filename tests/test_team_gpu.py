@@ -59,9 +59,11 @@ def run_case(name, T, n, Hb, Wb, seed=0, scale=0.05, wpc=1):
     ("tiny_ks3111", 1, 4, None), ("tiny_ks3111", 3, 5, None), ("tiny_ks3311", 8, 3, None),
     ("b8_lowrate_2rows", 8, 32, (2, 96)), ("b8_lowrate_2rows", 2, 40, (2, 20)), ("b8_lowrate_2rows", 5, 48, (2, 9)),
     ("b8_lowrate_2rows", 8, 64, (2, 5)), ("b8_lowrate_2rows", 3, 50, (2, 6)), ("b8_lowrate_2rows", 2, 96, (2, 4)),
+    ("b8_lowrate_2rows", 16, 32, (2, 6)), ("tiny_ks3311", 12, 3, None), ("b8_lowrate_2rows", 9, 40, (2, 5)),
 ])
 def test_team_equals_graph_decoder(name, T, n, shape, monkeypatch):
-    """Image counts of one to six row tiles, 1-8 teams.  64 images on a team of 32 workgroups (the bench's two-batch
+    """Image counts of one to six row tiles, 1-16 teams (9-16: two teams per XCD, each half its CUs; 12 and 9: XCD
+    slots with one team and with two).  64 images on a team of 32 workgroups (the bench's two-batch
     teams): up to 9 output tiles per workgroup on the fast path and two rANS waves per workgroup, each keeping its
     image's coder state in LDS; 50: some workgroups with one image; 96: three images per workgroup (each rANS wave
     decodes its rows one after another) and six row tiles (the long GEMM path)."""

@@ -48,12 +48,13 @@ def main():
         print(json.dumps(dict(decoder="graph", batches=1, seconds=round(tg, 4), ms_per_batch=round(tg * 1e3, 2))),
               flush=True)
     for T in Ts:
-        zs = decompress_teams(hs, [st] * T, Hb, Wb, wg_per_cu=int(os.environ.get("WPC", "1")))      # warm (records the program)
+        tsz = int(os.environ.get("TEAM_SIZE", "0"))
+        zs = decompress_teams(hs, [st] * T, Hb, Wb, wg_per_cu=int(os.environ.get("WPC", "1")), team_size=tsz)  # warm
         ok = all(torch.equal(zz, r["zhat"]) for zz in zs)
         os.environ["LBIC_TEAM_STAMPS"] = "1"
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        zs = decompress_teams(hs, [st] * T, Hb, Wb, wg_per_cu=int(os.environ.get("WPC", "1")))
+        zs = decompress_teams(hs, [st] * T, Hb, Wb, wg_per_cu=int(os.environ.get("WPC", "1")), team_size=tsz)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         os.environ["LBIC_TEAM_STAMPS"] = "0"
