@@ -91,6 +91,10 @@ def parse_args(argv=None):
                     help="team schedule: encoded 32-frame batches per decode team (2: each team of a launch decodes the "
                          "64 images of two batches side by side, 4 row tiles per weight fetch; a launch then holds up "
                          "to 2 x TEAM batches)")
+    ap.add_argument("--first-team-size", type=int, default=12,
+                    help="team schedule: workgroups per XCD slot of each team in the FIRST decode launch, the one beside "
+                         "the encoder's next batches (12 of the 32 CUs of every XCD, the rest left to the encoder; 0: all; "
+                         "LBC_OPT_TEAM_SIZE)")
     ap.add_argument("--first-team-batches", type=int, default=0, choices=(0, 1, 2),
                     help="team schedule: batches per team in the FIRST decode launch (0: --team-batches)")
     ap.add_argument("--team-sizes", default="",
@@ -429,7 +433,8 @@ def main():
                                 # (two workgroups per CU for the last launch measured slower:
                                 # profiles/r02_exp/team_two_per_cu.txt)
                                 zt = decompress_teams(dec_models[:len(tsts)], tsts, Hb, Wb,
-                                                      wg_per_cu=args.drain_wg_per_cu if last else 1)
+                                                      wg_per_cu=args.drain_wg_per_cu if last else 1,
+                                                      team_size=args.first_team_size if gi == 1 and not last else 0)
                                 sd_.synchronize()
                             zs = [z_[e * n:(e + 1) * n] for z_ in zt for e in range(tb_)]
                             with plock:
