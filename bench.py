@@ -87,10 +87,11 @@ def parse_args(argv=None):
                          "batches are decoded by ONE persistent team launch each (lbc_decode_team: one team of "
                          "workgroups per 32-frame batch; more than 8: two teams per XCD); 0 = the --workers / --depth "
                          "schedules")
-    ap.add_argument("--team-batches", type=int, default=1, choices=(1, 2),
-                    help="team schedule: encoded 32-frame batches per decode team (2: each team of a launch decodes the "
-                         "64 images of two batches side by side, 4 row tiles per weight fetch; a launch then holds up "
-                         "to 2 x TEAM batches)")
+    ap.add_argument("--team-batches", type=int, default=0, choices=(0, 1, 2),
+                    help="team schedule: encoded batches per decode team (2: each team of a launch decodes the images "
+                         "of two batches side by side, twice the row tiles per weight fetch; a launch then holds up to "
+                         "2 x TEAM batches; 0 = auto: 2 for batches of at most 16 frames, else 1 -- the headline's "
+                         "32-frame batches are decoded one per team)")
     ap.add_argument("--first-team-size", type=int, default=12,
                     help="team schedule: workgroups per XCD slot of each team in the FIRST decode launch, the one beside "
                          "the encoder's next batches (12 of the 32 CUs of every XCD, the rest left to the encoder; 0: all; "
@@ -133,7 +134,10 @@ def parse_args(argv=None):
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.team_batches == 0:
+        a.team_batches = 2 if a.batch <= 16 else 1
+    return a
 
 
 def relaunch_distributed(args):
