@@ -135,3 +135,15 @@ def test_bench_roofline_dominance_is_wall_occupancy():
     team["ms"] = 2000.0
     roof, _ = bench.roofline(kstats, dt, team, enc, steps)
     assert roof["kernel"] == "k_gemm_t" and roof["bound"] == "mfma"
+
+
+def test_bench_team_schedule_defaults():
+    """The headline's team schedule (bench.py defaults): 16 teams per launch, ONE 32-frame batch per team (each decode
+    pass decodes exactly one batch of the config), the first launch beside the encoder on 12 of every XCD's CUs; two
+    batches per team only for batches of at most 16 frames (configs 3 and 5)."""
+    import bench
+    a = bench.parse_args([])
+    assert (a.team, a.team_batches, a.first_team_size, a.batch) == (16, 1, 12, 32)
+    assert bench.parse_args(["--batch", "8"]).team_batches == 2
+    assert bench.parse_args(["--batch", "24"]).team_batches == 1
+    assert bench.parse_args(["--team-batches", "2"]).team_batches == 2
