@@ -712,10 +712,15 @@ def main():
                 "(no checkpoints / Kodak offline)",
         "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
                                f"in the reference bitstream format (one raster rANS stream per image); "
-                               + (f"each batch encoded as its own {n}-frame wavefront pass; decode: one persistent launch "
-                                  f"per group of up to {args.team * tb_cfg} batches, {tb_cfg} batch(es) per team of "
-                                  f"workgroups ({n * tb_cfg} images per team side by side), up to {args.team} teams per "
-                                  "launch (one per XCD up to 8, two per XCD beyond)" if args.team else
+                               + ((f"each batch encoded as its own {n}-frame wavefront pass and decoded as its own "
+                                   f"{n}-frame raster pass by one team of workgroups; up to {args.team} passes in one "
+                                   "persistent launch (one team per XCD up to 8, two per XCD beyond)"
+                                   if tb_cfg == 1 else
+                                   f"each batch encoded as its own {n}-frame wavefront pass; decode: {tb_cfg} batches per "
+                                   f"team of workgroups ({n * tb_cfg} images per team side by side), up to {args.team} "
+                                   "teams per launch")
+                                  + (f"; the first launch (beside the encoder's next batches) on {args.first_team_size} "
+                                     "of every XCD's 32 CUs" if args.first_team_size else "") if args.team else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
                                   f"up to {args.workers} passes in flight (one per worker)" if args.workers else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
@@ -725,9 +730,10 @@ def main():
                    "decode_passes_in_flight": args.team or args.workers or depth,
                    "frames_per_encode_pass": n * (args.enc_pass if args.team else 1),
                    "schedule": (f"team: one encoder handle (own HIP stream) compresses batch after batch, host rANS on "
-                                f"helper threads; every {args.team * tb_cfg} encoded batches are decoded by ONE persistent "
-                                "k_dec_team launch on a second stream (lbc_decode_team: a team of workgroups per "
-                                f"{tb_cfg} batch(es), team barriers instead of kernel boundaries), beside the next encodes"
+                                f"helper threads; every {args.team * tb_cfg} encoded batches (the first group: the "
+                                "remainder) are decoded by ONE persistent k_dec_team launch on a second stream "
+                                f"(lbc_decode_team: a team of workgroups per {'batch' if tb_cfg == 1 else f'{tb_cfg} batches'}, "
+                                "team barriers instead of kernel boundaries), beside the next encodes"
                                 if args.team else
                                 f"workers: {args.workers} codec handles on one weight set, each with its own HIP stream "
                                 "and host thread, take the batches in turn and compress, entropy code (host rANS) and "
