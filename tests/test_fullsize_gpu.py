@@ -182,7 +182,8 @@ def test_gang_past_int32_offsets():
 
 
 TEAM_FULL = {   # (arch, H, W, batches, frames per batch, rate): every config's frame size through the team decoder
-    "B8_lowrate": ((8, (3, 1, 1, 1), 768, 96), 768, 768, 8, 32, "low"),      # the headline's 8-batch launch
+    "B8_lowrate": ((8, (3, 1, 1, 1), 768, 96), 768, 768, 8, 32, "low"),      # round 4's 8-batch launch
+    "B8_lowrate_16": ((8, (3, 1, 1, 1), 768, 96), 768, 768, 16, 32, "low"),  # the headline's 16-batch launch
     "B8_highrate": ((8, (3, 3, 1, 1), 1152, 128), 512, 768, 3, 3, "high"),
     "B4_highrate": ((4, (3, 3, 1, 1), 512, 96), 768, 768, 2, 2, "high"),
     "B16_lowrate": ((16, (3, 1, 1, 1), 1280, 192), 2048, 2048, 2, 2, "low"),
@@ -194,9 +195,9 @@ TEAM_FULL = {   # (arch, H, W, batches, frames per batch, rate): every config's 
 
 @pytest.mark.parametrize("name", sorted(TEAM_FULL))
 def test_team_full_size_roundtrip(name):
-    """lbc_decode_team at every config's real frame size (the headline's shape: 8 batches of 32 768x768 frames in
-    one launch): every batch decodes bit-exactly to the encoder's reconstruction, with the rANS variant the rate
-    calls for (sparse below 1 bit per symbol, the dense one with its tables in LDS above)."""
+    """lbc_decode_team at every config's real frame size (the headline's shape: 16 batches of 32 768x768 frames in
+    one launch, two teams per XCD): every batch decodes bit-exactly to the encoder's reconstruction, with the rANS
+    variant the rate calls for (sparse below 1 bit per symbol, the dense one with its tables in LDS above)."""
     from lbic.arch import Arch
     from lbic.model import decompress_teams
     (B, KS, N, M), H, W, T, n, rate = TEAM_FULL[name]

@@ -86,7 +86,7 @@ def test_team_full_frame_in_headline_launch(monkeypatch):
     Hb, Wb = H // arch.B, W // arch.B
     img = np.random.default_rng(int(g["image_seed"])).integers(0, 256, (1, 3, H, W), dtype=np.uint8)[0]
     assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["image_sha256"])
-    T, n = 8, 32
+    T, n = 16, 32          # the headline's launch: 16 batches of 32 frames, two teams per XCD
     hs = _handles(arch, int(g["weight_seed"]), str(g["rate"]), T)
     m = hs[0]
     xb = torch.from_numpy(image_to_blocks(img.astype(np.float32) / 255.0 - 0.5, arch.B))[None].cuda()
