@@ -123,5 +123,5 @@ def test_team_full_frame_in_headline_launch(monkeypatch):
         assert dz <= 1e-5 * float(np.abs(zr).max()), f"team {t}: zhat rows differ from the reference by {dz}"
         assert dsum <= 1e-5 * float(np.abs(z).sum(-1).max()), f"team {t}: block sums differ by {dsum}"
         assert torch.equal(got[t][t], r["zhat"][0])
-    print(f"headline launch: fixture frame in 8 teams, max |dzhat| rows {dz:.3e}, block sums {dsum:.3e}, "
+    print(f"headline launch: fixture frame in {T} teams, max |dzhat| rows {dz:.3e}, block sums {dsum:.3e}, "
           f"{len(flips)} scale-index flips at listed near ties")
