@@ -243,10 +243,17 @@ struct lbc_model {
 
 namespace {
 
-int dev_upload(DevBuf& d, const void* src, size_t bytes) {
+int dev_upload(DevBuf& d, const void* src, size_t bytes, hipStream_t s = nullptr) {
     int rc = d.alloc(bytes);
     if (rc) return rc;
-    HIPCHK(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
+    if (!s) {
+        HIPCHK(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
+        return LBC_OK;
+    }
+    // on a non-blocking stream of the handle: a legacy-stream copy fails while another thread of the process captures
+    // a graph (decoder handles sizing their workspaces beside each other's first captures)
+    HIPCHK(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
     return LBC_OK;
 }
 
@@ -414,10 +421,10 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
             return set_error(LBC_E_ARG, "frame batch too large (layer-0 cache above 64 GB); split the batch");
     }
     int rc;
-    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4)))) return rc;
-    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4)))) return rc;
+    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4), m->cap2))) return rc;
+    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4), m->cap2))) return rc;
     if (m->l0_on) {
-        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4)))) return rc;
+        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4), m->cap2))) return rc;
         const size_t b = (size_t)n_img * (Hb + 2) * (Wb + 4) * m->C1P * sizeof(float);
         if ((rc = m->l0.alloc(b))) return rc;
         if ((rc = ws_zero(m, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
@@ -1681,8 +1688,10 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     }
     const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
     if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
-    HIPCHK(hipMemcpy(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice));
+    hipStream_t us = m0->cap2;     // (a legacy-stream copy fails while another thread captures a graph)
+    HIPCHK(hipMemcpyAsync(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice, us));
+    HIPCHK(hipMemcpyAsync(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice, us));
+    HIPCHK(hipStreamSynchronize(us));
     if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 2) * 32 * sizeof(unsigned)))) return rc;
     if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
     TeamArgs& a = m0->team_args;
