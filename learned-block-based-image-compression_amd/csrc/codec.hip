@@ -243,15 +243,15 @@ struct lbc_model {
 
 namespace {
 
-int dev_upload(DevBuf& d, const void* src, size_t bytes, hipStream_t s = nullptr) {
+int dev_upload(DevBuf& d, const void* src, size_t bytes, hipStream_t s = nullptr, bool on_s = false) {
     int rc = d.alloc(bytes);
     if (rc) return rc;
-    if (!s) {
+    if (!on_s) {
         HIPCHK(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
         return LBC_OK;
     }
-    // on a non-blocking stream of the handle: a legacy-stream copy fails while another thread of the process captures
-    // a graph (decoder handles sizing their workspaces beside each other's first captures)
+    // on the caller's stream (ordered after its earlier work), then waited for: a legacy-stream copy fails while another
+    // thread of the process captures a graph (decoder handles sizing their workspaces beside each other's captures)
     HIPCHK(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     return LBC_OK;
@@ -354,21 +354,16 @@ int pack_gdn(lbc_model* m, Layer& L, const std::string& name, int C) {
     return upload_layer(L, wkn, beta, pad16(C), C);
 }
 
-// zero a fresh workspace buffer on the handle's non-blocking stream and wait for it: a hipMemset on the legacy stream
-// fails while another thread of the process captures a graph (a decoder handle sizing its workspace beside another
-// handle's first row-graph capture, bench.py's sub-stream leg)
-static int ws_zero(lbc_model* m, void* p, size_t b) {
-    hipStream_t z = m->cap2;
-    if (!z) {
-        HIPCHK(hipMemset(p, 0, b));
-        return LBC_OK;
-    }
-    HIPCHK(hipMemsetAsync(p, 0, b, z));
-    HIPCHK(hipStreamSynchronize(z));
+// zero a fresh workspace buffer on the caller's stream s (ordered after its earlier work) and wait for it: a
+// hipMemset on the legacy stream fails while another thread of the process captures a graph (decoder handles sizing
+// their workspaces beside each other's first row-graph captures, bench.py's sub-stream leg); s = 0 is that legacy stream
+static int ws_zero(hipStream_t s, void* p, size_t b) {
+    HIPCHK(hipMemsetAsync(p, 0, b, s));
+    HIPCHK(hipStreamSynchronize(s));
     return LBC_OK;
 }
 
-int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
+int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb, hipStream_t s) {
     if (m->ws_n == n_img && m->ws_Hb == Hb && m->ws_Wb == Wb) return LBC_OK;
     const int T = (Wb - 1) + 2 * (Hb - 1) + 1;
     std::vector<int4> enc;
@@ -421,13 +416,13 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
             return set_error(LBC_E_ARG, "frame batch too large (layer-0 cache above 64 GB); split the batch");
     }
     int rc;
-    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4), m->cap2))) return rc;
-    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4), m->cap2))) return rc;
+    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4), s, true))) return rc;
+    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4), s, true))) return rc;
     if (m->l0_on) {
-        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4), m->cap2))) return rc;
+        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4), s, true))) return rc;
         const size_t b = (size_t)n_img * (Hb + 2) * (Wb + 4) * m->C1P * sizeof(float);
         if ((rc = m->l0.alloc(b))) return rc;
-        if ((rc = ws_zero(m, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
+        if ((rc = ws_zero(s, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
     }
     const size_t F = sizeof(float);
     if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
@@ -444,7 +439,7 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb) {
         for (int i = 0; i < 10; ++i) {
             if (l > 0 && (i == 4 || i == 5)) continue;   // encoder-only buffers
             if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
-            if ((rc = ws_zero(m, bufs[i]->p, rows * widths[i] * F))) return rc;
+            if ((rc = ws_zero(s, bufs[i]->p, rows * widths[i] * F))) return rc;
         }
     }
     m->Mmax = mmax;
@@ -1037,7 +1032,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if ((rc = prepare_device(m))) return rc;
-    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb, s))) return rc;
     const size_t nx = (size_t)n_img * Hb * Wb * m->Cx, nsym = (size_t)n_img * Hb * Wb * m->M;
     if ((rc = m->x_in.alloc(nx * 4)) || (rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4)) ||
         (rc = m->bits_buf.alloc(nsym * 4)))
@@ -1128,7 +1123,7 @@ int lbc_band_begin(lbc_model* m, const float* x_dev, int n_img, int Hb_band, int
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if ((rc = prepare_device(m))) return rc;
-    if ((rc = ensure_workspace(m, n_img, Hb_band, Wb))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb_band, Wb, s))) return rc;
     const size_t nx = (size_t)n_img * Hb_band * Wb * m->Cx, nsym = (size_t)n_img * Hb_band * Wb * m->M;
     if ((rc = m->x_in.alloc(nx * 4)) || (rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4)) ||
         (rc = m->bits_buf.alloc(nsym * 4)))
@@ -1223,7 +1218,7 @@ int lbc_forward(lbc_model* m, const float* x_dev, const float* zhat_dev, int n_i
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if ((rc = prepare_device(m))) return rc;
-    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb, s))) return rc;
     const size_t nsym = (size_t)n_img * Hb * Wb * m->M;
     if ((rc = m->sym_buf.alloc(nsym * 4)) || (rc = m->idx_buf.alloc(nsym * 4))) return rc;
     // teacher forcing: the given zhat is the reconstruction every block sees (zero border as before)
@@ -1479,7 +1474,7 @@ int lbc_decode(lbc_model* m, const uint8_t* const* streams, const size_t* lens, 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if ((rc = prepare_device(m))) return rc;
-    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb, s))) return rc;
     std::vector<std::pair<const uint8_t*, size_t>> subs;
     for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[i], lens[i]);
     if ((rc = upload_streams(m, subs, s))) return rc;
@@ -1636,7 +1631,8 @@ static int team_fallback(lbc_model* const* ms, int T, const uint8_t* const* stre
 // The team program (held by ms[0]): every team's raster step recorded from the same run_ctx / run_dec calls that build
 // the graph decoder, for the geometry (S, spread); rebuilt when the geometry, any team's buffers or any team's
 // weight set (Net::gen) changed.  Sets ms[0]->team_args (without the per-launch fields) and the step's algorithmic work.
-static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, int S, int spread, int sparse) {
+static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, int S, int spread, int sparse,
+                       hipStream_t us) {
     lbc_model* m0 = ms[0];
     int rc;
     std::vector<long long> key = {T, S, spread, n_img, Hb, Wb, sparse};
@@ -1688,7 +1684,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     }
     const size_t gb = gem.size() * sizeof(GemmArgs), rb = rans.size() * sizeof(RansArgs);
     if ((rc = m0->team_prog.alloc(gb + rb))) return rc;
-    hipStream_t us = m0->cap2;     // (a legacy-stream copy fails while another thread captures a graph)
+    // (on the launch's stream: a legacy-stream copy fails while another thread captures a graph)
     HIPCHK(hipMemcpyAsync(m0->team_prog.p, gem.data(), gb, hipMemcpyHostToDevice, us));
     HIPCHK(hipMemcpyAsync(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice, us));
     HIPCHK(hipStreamSynchronize(us));
@@ -1802,7 +1798,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     for (int t = 0; t < T; ++t) {
         lbc_model* m = ms[t];
         if ((rc = prepare_device(m))) return rc;
-        if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+        if ((rc = ensure_workspace(m, n_img, Hb, Wb, s))) return rc;
         if ((rc = m->ctr.alloc(kLanes * sizeof(int)))) return rc;
         std::vector<std::pair<const uint8_t*, size_t>> subs;
         for (int i = 0; i < n_img; ++i) subs.emplace_back(streams[(size_t)t * n_img + i], lens[(size_t)t * n_img + i]);
@@ -1831,7 +1827,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
         }
         S *= spread;
         if (S < 1) return team_fallback(ms, T, streams, lens, n_img, Hb, Wb, zhat_devs, stream);
-        if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse))) return rc;
+        if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse, s))) return rc;
         a = m0->team_args;
         // high rates: the tables staged in every workgroup's LDS (rans_row<true>); low rates: rans_row_sparse, its rare
         // far symbols searched in the table image in global memory
@@ -1841,7 +1837,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
             // the dense tables do not fit beside this geometry's partials (high rates with many tiles per workgroup):
             // the sparse coder -- tables read from global memory, any rate, bit-identical -- instead of the row graphs
             sparse = 1;
-            if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse))) return rc;
+            if ((rc = team_record(ms, T, n_img, Hb, Wb, S, spread, sparse, s))) return rc;
             a = m0->team_args;
             a.dense = 0;
             lds = team_lds_bytes(a);
@@ -2007,7 +2003,7 @@ int lbc_decode_rows(lbc_model* m, const uint8_t* const* streams, const size_t* l
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if ((rc = prepare_device(m))) return rc;
-    if ((rc = ensure_workspace(m, n_img, Hb, Wb))) return rc;
+    if ((rc = ensure_workspace(m, n_img, Hb, Wb, s))) return rc;
     std::vector<std::pair<const uint8_t*, size_t>> subs;       // stream (img, v) at img * Hb + v
     for (int i = 0; i < n_img; ++i) {
         uint32_t hdr[2];
