@@ -11,11 +11,13 @@ rANS decode).  Every batch is encoded as its own 32-frame wavefront pass and dec
 Schedule of the headline (`value`, `--team 16`, the default): one encoder handle compresses batch after batch on its
 own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the remainder) are decoded
 by ONE persistent k_dec_team launch (lbc_decode_team: one team of workgroups per 32-frame batch, two teams per XCD,
-team barriers instead of kernel boundaries) on a second stream, beside the encoder's next batches.  `--team 0` selects the `--workers` schedule (W codec handles on the
-shared weights, each compressing, entropy coding and decoding whole batches) or, with `--workers 0`, the encoder +
-`--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
+team barriers instead of kernel boundaries) on a second stream, beside the encoder's next batches; the first launch
+runs on 12 of every XCD's 32 CUs (`--first-team-size`), the rest left to the encoder.  `--team 0` selects the
+`--workers` schedule (W codec handles on the shared weights, each compressing, entropy coding and decoding whole
+batches) or, with `--workers 0`, the encoder + `--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
 decompressions of the same batches, fill and drain included; inputs are resident in HBM when it starts.  Reported
-beside it: one decode pass in flight (`one_decode_in_flight`), no overlap at all (`serial_schedule`), the gang
+beside it: the same schedule with 8 whole-XCD teams per launch (`eight_teams_per_launch`), one decode pass in flight
+(`one_decode_in_flight`), no overlap at all (`serial_schedule`), the gang
 schedule (`gang_schedule`: one raster pass over several queued batches, more frames in flight, not the headline),
 and the opt-in sub-stream format (`substream_format`, not the reference bitstream).
 
