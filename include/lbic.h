@@ -138,7 +138,13 @@ int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_
  * rANS stream per image); images are decoded together, rANS decode runs on the GPU.  The streams are
  * copied to the device in `stream` order (after that stream's earlier work).  The call is synchronous:
  * it returns after the whole decode has finished on `stream` (it reads back the per-stream status to
- * report a corrupt bitstream), so the caller may free or reuse its buffers on return. */
+ * report a corrupt bitstream), so the caller may free or reuse its buffers on return.
+ * Stream integrity (stricter than CompressAI's RansDecoder, which never checks): LBC_E_STREAM when a stream runs out
+ * of words before its last block (truncated), or when its coder state after the last block is not the encoder's
+ * initial state 2^31 (Rans64EncInit; the decoder retraces the encoder's states in reverse), which a corrupted stream
+ * misses with near certainty.  Words after the last one the decode reads (trailing padding) are ignored, as the
+ * reference's decoder ignores them.  Every decoder path (row graphs, k_dec_one, lbc_decode_team, lbc_decode_rows)
+ * applies the same check. */
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 /* How the last lbc_decode of this handle ran (no reference counterpart: a query for tests and the bench).  *path: 0

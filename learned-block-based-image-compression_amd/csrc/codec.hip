@@ -210,6 +210,10 @@ struct lbc_model {
     // encoder transform's first six GEMMs on cap; the quantising GEMM joins both
     hipStream_t cap2 = nullptr;
     hipEvent_t fev[2] = {nullptr, nullptr};
+    // workspace set-up (ws_zero / dev_upload with a handle): a private non-blocking stream ordered after the caller's stream by
+    // an event, never the legacy stream
+    hipStream_t aux = nullptr;
+    hipEvent_t aux_ev = nullptr;
     // band pipeline (lbc_band_*): this handle codes block rows [band_v0, band_v0 + ws_Hb) of taller frames;
     // one captured graph per range of global wavefront steps
     int band_v0 = -1;
@@ -243,17 +247,31 @@ struct lbc_model {
 
 namespace {
 
-int dev_upload(DevBuf& d, const void* src, size_t bytes, hipStream_t s = nullptr, bool on_s = false) {
+// workspace set-up stream of handle m, ordered after the caller's stream s (an event recorded on s, waited for by the
+// handle's private non-blocking stream): a legacy-stream memset / copy fails while another thread of the process
+// captures a graph (decoder handles sizing their workspaces beside each other's captures), and a plain non-blocking
+// stream without the event raced the handle's previous encode still running on s (round 5, test_batch_equals_single)
+hipStream_t ws_stream(lbc_model* m, hipStream_t s) {
+    if (!m->aux) return nullptr;
+    if (hipEventRecord(m->aux_ev, s) != hipSuccess || hipStreamWaitEvent(m->aux, m->aux_ev, 0) != hipSuccess) {
+        set_error(LBC_E_HIP, "workspace stream ordering failed");
+        return nullptr;
+    }
+    return m->aux;
+}
+
+int dev_upload(DevBuf& d, const void* src, size_t bytes, lbc_model* m = nullptr, hipStream_t s = nullptr) {
     int rc = d.alloc(bytes);
     if (rc) return rc;
-    if (!on_s) {
+    if (!m) {
         HIPCHK(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
         return LBC_OK;
     }
-    // on the caller's stream (ordered after its earlier work), then waited for: a legacy-stream copy fails while another
-    // thread of the process captures a graph (decoder handles sizing their workspaces beside each other's captures)
-    HIPCHK(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
+    // on the handle's set-up stream (after the caller's earlier work on s), then waited for
+    hipStream_t q = ws_stream(m, s);
+    if (!q) return set_error(LBC_E_HIP, "workspace stream unavailable");
+    HIPCHK(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, q));
+    HIPCHK(hipStreamSynchronize(q));
     return LBC_OK;
 }
 
@@ -354,12 +372,13 @@ int pack_gdn(lbc_model* m, Layer& L, const std::string& name, int C) {
     return upload_layer(L, wkn, beta, pad16(C), C);
 }
 
-// zero a fresh workspace buffer on the caller's stream s (ordered after its earlier work) and wait for it: a
-// hipMemset on the legacy stream fails while another thread of the process captures a graph (decoder handles sizing
-// their workspaces beside each other's first row-graph captures, bench.py's sub-stream leg); s = 0 is that legacy stream
-static int ws_zero(hipStream_t s, void* p, size_t b) {
-    HIPCHK(hipMemsetAsync(p, 0, b, s));
-    HIPCHK(hipStreamSynchronize(s));
+// zero a fresh workspace buffer on the handle's set-up stream (ordered after the caller's earlier work on s, ws_stream)
+// and wait for it
+static int ws_zero(lbc_model* m, hipStream_t s, void* p, size_t b) {
+    hipStream_t q = ws_stream(m, s);
+    if (!q) return set_error(LBC_E_HIP, "workspace stream unavailable");
+    HIPCHK(hipMemsetAsync(p, 0, b, q));
+    HIPCHK(hipStreamSynchronize(q));
     return LBC_OK;
 }
 
@@ -416,13 +435,13 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb, hipStream_t s) {
             return set_error(LBC_E_ARG, "frame batch too large (layer-0 cache above 64 GB); split the batch");
     }
     int rc;
-    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4), s, true))) return rc;
-    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4), s, true))) return rc;
+    if ((rc = dev_upload(m->blocks_enc, enc.data(), enc.size() * sizeof(int4), m, s))) return rc;
+    if ((rc = dev_upload(m->blocks_dec, dec.data(), dec.size() * sizeof(int4), m, s))) return rc;
     if (m->l0_on) {
-        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4), s, true))) return rc;
+        if ((rc = dev_upload(m->cells_enc, cells.data(), cells.size() * sizeof(int4), m, s))) return rc;
         const size_t b = (size_t)n_img * (Hb + 2) * (Wb + 4) * m->C1P * sizeof(float);
         if ((rc = m->l0.alloc(b))) return rc;
-        if ((rc = ws_zero(s, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
+        if ((rc = ws_zero(m, s, m->l0.p, b))) return rc;   // pad channels stay 0 (never written; A x 0-weight meets no NaN)
     }
     const size_t F = sizeof(float);
     if ((rc = m->zpad.alloc((size_t)n_img * (Hb + 2) * (Wb + 4) * m->Cx * F))) return rc;
@@ -439,7 +458,7 @@ int ensure_workspace(lbc_model* m, int n_img, int Hb, int Wb, hipStream_t s) {
         for (int i = 0; i < 10; ++i) {
             if (l > 0 && (i == 4 || i == 5)) continue;   // encoder-only buffers
             if ((rc = bufs[i]->alloc(rows * widths[i] * F))) return rc;
-            if ((rc = ws_zero(s, bufs[i]->p, rows * widths[i] * F))) return rc;
+            if ((rc = ws_zero(m, s, bufs[i]->p, rows * widths[i] * F))) return rc;
         }
     }
     m->Mmax = mmax;
@@ -460,6 +479,8 @@ int prepare_device(lbc_model* m) {
         HIPCHK(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&m->cap2, hipStreamNonBlocking));
         for (auto& e : m->fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&m->aux_ev, hipEventDisableTiming));
     }
     if (m->tabs_dirty) {
         int rc;
@@ -614,8 +635,9 @@ int rans_sparse_choice(const size_t* lens, int n, double symbols) {
 }
 
 // full: the decode consumed every block of every stream, so each rANS stream must end where its encoder began: state
-// RANS64_L = 2^31 (Rans64EncInit; the decoder retraces the encoder's states in reverse) with every word read.  A
-// truncated stream overruns (status); a corrupted one ends in another state with near certainty -- both raise.
+// RANS64_L = 2^31 (Rans64EncInit; the decoder retraces the encoder's states in reverse).  A truncated stream overruns
+// (status); a corrupted one ends in another state with near certainty -- both raise.  Words past the last one read
+// (trailing padding) are ignored, as CompressAI's RansDecoder ignores them (lbic.h, lbc_decode).
 int check_status(lbc_model* m, size_t n, hipStream_t s, bool full) {
     std::vector<int> status(n), ptr(full ? n : 0), cnt(full ? n : 0);
     std::vector<unsigned long long> x(full ? n : 0);
@@ -628,7 +650,7 @@ int check_status(lbc_model* m, size_t n, hipStream_t s, bool full) {
     HIPCHK(hipStreamSynchronize(s));
     for (size_t i = 0; i < n; ++i) {
         if (status[i]) return set_error(LBC_E_STREAM, "corrupt bitstream (stream " + std::to_string(i) + ")");
-        if (full && (x[i] != (1ull << 31) || ptr[i] != cnt[i]))
+        if (full && (x[i] != (1ull << 31) || ptr[i] > cnt[i]))
             return set_error(LBC_E_STREAM, "corrupt bitstream (stream " + std::to_string(i) +
                                                ": the decode does not end in the encoder's initial state)");
     }
@@ -918,6 +940,8 @@ void lbc_destroy(lbc_model* m) {
     if (m->cap2) (void)hipStreamDestroy(m->cap2);
     for (auto e : m->fev)
         if (e) (void)hipEventDestroy(e);
+    if (m->aux) (void)hipStreamDestroy(m->aux);
+    if (m->aux_ev) (void)hipEventDestroy(m->aux_ev);
     delete m;
 }
 

@@ -106,3 +106,30 @@ def test_transform_weights_are_a_codec():
     assert psnr > 28 and bpp < 1.5, (psnr, bpp)
     with pytest.raises(ValueError):
         transform_state_dict(Arch(4, (3, 3, 1, 1), 512, 96))    # 96 coefficients > 3 * 4^2
+
+
+def test_bench_team_group_sizes():
+    """bench.py's team schedule never asks for more teams than one launch holds: odd batch counts at two
+    batches per team and one batch per team on a full group are split; explicit --team-sizes are validated."""
+    import bench
+    f = bench.team_group_sizes
+    assert f(20, 16, 1) == [4, 16]                       # the driver's command: partial group first
+    assert f(32, 16, 1) == [16, 16]
+    assert f(17, 16, 2) == [1, 16]                       # 17 at two per team would be 17 one-batch teams
+    assert f(33, 16, 2) == [1, 32]
+    assert f(32, 16, 2, first_tb=1) == [16, 16]          # --first-team-batches 1 on a full group of 32
+    assert f(10, 16, 2, order="first-full") == [10]
+    for steps in range(1, 70):
+        for tb in (1, 2):
+            for first in (0, 1, 2):
+                sizes = f(steps, 16, tb, first_tb=first)
+                assert sum(sizes) == steps
+                for i, s in enumerate(sizes):
+                    t = first if i == 0 and first else tb
+                    assert 1 <= (s // t if s % t == 0 else s) <= 16
+    with pytest.raises(SystemExit):
+        f(20, 16, 1, explicit="3,17")                    # 17 one-batch teams
+    with pytest.raises(SystemExit):
+        f(20, 16, 1, explicit="4,15")                    # does not sum to 20
+    assert f(20, 16, 1, explicit="4,16") == [4, 16]
+    assert bench.first_wg_per_xcd(4, 12) == 12 and bench.first_wg_per_xcd(16, 12) == 24

@@ -142,3 +142,36 @@ def test_one_bad_stream_raises(damage, monkeypatch):
     assert p["path"] == "one" and p["one_timeouts"] == t0, p
     assert torch.equal(m.decompress_batch([stream], Hb, Wb), good)
     assert m.decode_path()["path"] == "one"
+
+
+@pytest.mark.parametrize("path", ["one", "graphs", "team"])
+def test_trailing_padding_words_ignored(path, monkeypatch):
+    """Words after the last one a decode reads are ignored, as CompressAI's RansDecoder ignores them: a
+    reference-format stream with trailing zero words decodes to the same image through k_dec_one, the row graphs and a
+    team launch, while a corrupted last word still raises (the end-state check, lbic.h lbc_decode)."""
+    from lbic.model import decompress_teams
+    monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
+    g = load_golden("loop_tiny_ks3111")
+    arch = golden_arch(g)
+    Hb, Wb = g["x"].shape[:2]
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
+    padded = stream + bytes(8)
+    bad = bytearray(padded)
+    bad[len(stream) - 4:len(stream)] = bytes(b ^ 0xA5 for b in bad[len(stream) - 4:len(stream)])
+    if path == "team":
+        hs = [m, m.sibling()]
+        good = decompress_teams(hs, [[stream] * 2] * 2, Hb, Wb)
+        got = decompress_teams(hs, [[padded] * 2] * 2, Hb, Wb)
+        assert hs[0].team_stats()["mode"] == "team_sparse"
+        assert all(torch.equal(a, b) for a, b in zip(got, good))
+        with pytest.raises((RuntimeError, ValueError)):
+            decompress_teams(hs, [[padded, bytes(bad)]] * 2, Hb, Wb)
+        return
+    n = 1 if path == "one" else 2
+    good = m.decompress_batch([stream] * n, Hb, Wb)
+    assert torch.equal(m.decompress_batch([padded] * n, Hb, Wb), good)
+    assert m.decode_path()["path"] == path
+    assert_rel(good[0].cpu().numpy(), g["zhat_dec"], what="decoded zhat vs the reference's decompress()")
+    with pytest.raises((RuntimeError, ValueError)):
+        m.decompress_batch([bytes(bad)] * n, Hb, Wb)

@@ -76,6 +76,40 @@ def test_team_decodes_reference_stream(name, sparse, spread, monkeypatch):
     print(f"{name} spread={spread} sparse={sparse}: max |zhat - zhat_dec(ref)| = {worst:.3e} (bar {1e-5 * np.abs(ref).max():.3e})")
 
 
+@pytest.mark.parametrize("sparse", ["0", "1"])
+@pytest.mark.parametrize("name,n", [("tiny_ks3311", 32), ("b4_highrate_mid", 32), ("b8_highrate_mid", 32),
+                                    ("b16_lowrate_low", 32), ("b8_lowrate_2rows", 32),
+                                    ("b8_highrate_mid", 6), ("b16_lowrate_low", 16)])
+def test_team_reference_stream_headline_geometry(name, n, sparse, monkeypatch):
+    """The headline's launch geometry -- 16 teams, two per XCD slot (sub = 2), each half an XCD's CUs -- on the
+    reference's own stream at high rate, with the KS3311 layer-0 cache and at B16: n = 32 copies per team (one 32-frame
+    batch per team, configs 2 and 4), n = 6 (config 3's HEAD default: two 3-frame Kodak shards per team) and n = 16
+    (config 5's: two 8-frame batches per team).  Every image must equal the reference's decompress() output within
+    1e-5 relative and every copy be bit-identical.  The dense coder may give way to the sparse one where its tables do
+    not fit a workgroup's LDS beside the partials (bit-identical, lbc_decode_team); the row-graph fallback may not run."""
+    from lbic.model import decompress_teams
+    monkeypatch.setenv("LBIC_RANS_SPARSE", sparse)
+    monkeypatch.delenv("LBIC_TEAM_SPREAD", raising=False)
+    g = load_golden("loop_" + name)
+    arch = golden_arch(g)
+    Hb, Wb = g["x"].shape[:2]
+    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
+    T = 16
+    hs = _handles(arch, int(g["weight_seed"]), golden_rate(g), T)
+    got = decompress_teams(hs, [[stream] * n for _ in range(T)], Hb, Wb)
+    st = hs[0].team_stats()
+    assert st["mode"] in (("team_sparse",) if sparse == "1" else ("team_sparse", "team_dense")), st
+    assert st["plain"] == 1 and st["timeout_fallbacks"] == 0, st
+    ref = g["zhat_dec"]
+    assert_rel(got[0][0].cpu().numpy(), ref, what=f"{name} T=16 n={n} vs the reference's decompress()")
+    for t in range(T):
+        assert got[t].shape[0] == n
+        for i in range(n):
+            assert torch.equal(got[t][i], got[0][0]), f"team {t} image {i} differs from team 0 image 0"
+    print(f"{name} T=16 n={n} sparse={sparse} ({st['mode']}): max |zhat - zhat_dec(ref)| = "
+          f"{float(np.abs(got[0][0].cpu().numpy() - ref).max()):.3e}")
+
+
 def test_team_full_frame_in_headline_launch(monkeypatch):
     from lbic.layout import image_to_blocks
     from lbic.model import decompress_teams

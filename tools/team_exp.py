@@ -69,6 +69,9 @@ def main():
                 prev = row[k]
             ops.append(d)
             comp.append(c)
+        if os.environ.get("RAW_OUT"):      # every team's raw stamp block (offline decomposition)
+            with open(os.environ["RAW_OUT"] + f"_T{T}.json", "w") as f:
+                json.dump([[int(v) for v in row] for row in ts], f)
         span = [round((row[63] - row[62]) / 1e5, 2) for row in ts]
         step = [round((row[61] - row[60]) / 100.0, 2) for row in ts]
         print(json.dumps(dict(decoder="team", batches=T, seconds=round(dt, 4), ms_per_batch=round(dt * 1e3 / T, 2),
