@@ -174,11 +174,12 @@ int lbc_one_stamps(const lbc_model *m, unsigned long long *out, int max_out, int
  * Batches the team kernel does not cover (M > 256, buffers past 4 GB) are decoded by lbc_decode one after another.  Synchronous like lbc_decode; one call at a time per process. */
 int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *streams, const size_t *lens, int n_img,
                     int Hb, int Wb, float *const *zhat_devs, void *stream);
-/* raw stamps of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 256 per team (team rank 0), s_memrealtime
+/* raw stamps of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 1024 per team (team rank 0), s_memrealtime
  * (100 MHz): [op] after each barrier of the sampled raster step (Hb/2, Wb/2), [32 + op] when rank 0's own share of the
  * operation was done, [60] end of the step before it, [61] end of the sampled step, [62] launch start, [63] launch
- * end; s_memtime (shader clock) [64 + 8 op + p] inside the operation's GEMM (p: entry, loads issued, first chain, all
- * chains, outputs written).  m = the call's first handle. */
+ * end; s_memtime (shader clock) [256 + 32 op + p] inside the operation's GEMM (p: entry, A loads issued, first chain, all
+ * chains, outputs written, epilogue operands issued, first weights issued, offsets, partials reduced (8), first round
+ * of outputs written (9), wave w's chains done (16 + w), its first chain done (24 + w)).  m = the call's first handle. */
 int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 /* the last lbc_decode_team launch led by m: its duration (HIP events around the launch), algorithmic bytes and FLOPs
  * (per raster step, the graph decoder's accounting: weights + A rows + outputs once per GEMM, rANS inputs and

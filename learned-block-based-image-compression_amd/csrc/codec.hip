@@ -1713,7 +1713,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     HIPCHK(hipMemcpyAsync(static_cast<char*>(m0->team_prog.p) + gb, rans.data(), rb, hipMemcpyHostToDevice, us));
     HIPCHK(hipStreamSynchronize(us));
     if ((rc = m0->team_sync.alloc((size_t)(TEAM_MAX + 2) * 32 * sizeof(unsigned)))) return rc;
-    if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * 256 * sizeof(unsigned long long)))) return rc;
+    if ((rc = m0->team_ts.alloc((size_t)TEAM_MAX * TEAM_TS_WORDS * sizeof(unsigned long long)))) return rc;
     TeamArgs& a = m0->team_args;
     a = TeamArgs{};
     a.gemm = m0->team_prog.as<GemmArgs>();
@@ -1898,7 +1898,7 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     for (int attempt = 0; attempt < 2; ++attempt) {
         if ((rc = reset())) return rc;
         HIPCHK(hipMemsetAsync(m0->team_sync.p, 0, (size_t)(TEAM_MAX + 2) * 32 * sizeof(unsigned), s));
-        if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * 256 * sizeof(unsigned long long), s));
+        if (a.ts) HIPCHK(hipMemsetAsync(m0->team_ts.p, 0, (size_t)TEAM_MAX * TEAM_TS_WORDS * sizeof(unsigned long long), s));
         HIPCHK(hipEventRecord(m0->ev[2], s));
         if ((rc = launch_dec_team(a, s))) return rc;
         HIPCHK(hipEventRecord(m0->ev[3], s));
@@ -1929,13 +1929,14 @@ int lbc_decode_team(lbc_model* const* ms, int n_teams, const uint8_t* const* str
     for (int t = 0; t < T; ++t)
         if ((rc = launch_copy_interior(ms[t]->zpad.as<float>(), zhat_devs[t], n_img, Hb, Wb, ms[t]->Cx, s))) return rc;
     if (a.ts) {
-        m0->team_ts_host.assign((size_t)T * 256, 0ull);
-        HIPCHK(hipMemcpyAsync(m0->team_ts_host.data(), m0->team_ts.p, (size_t)T * 256 * sizeof(unsigned long long),
+        m0->team_ts_host.assign((size_t)T * TEAM_TS_WORDS, 0ull);
+        HIPCHK(hipMemcpyAsync(m0->team_ts_host.data(), m0->team_ts.p, (size_t)T * TEAM_TS_WORDS * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     if (const char* e = getenv("LBIC_TEAM_VERBOSE"); e && atoi(e))
-        fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d\n", T, S, a.plain, m0->team_fallbacks);
+        fprintf(stderr, "[lbic] team decode: T=%d S=%d plain=%d reruns=%d lds=%zu\n", T, S, a.plain, m0->team_fallbacks,
+                team_lds_bytes(a));
     for (int t = 0; t < T; ++t)
         if ((rc = check_status(ms[t], (size_t)n_img, s, true))) return rc;
     return LBC_OK;

@@ -108,6 +108,7 @@ struct RansArgs {
 constexpr int TEAM_SLOTS = 8;      // XCD slots of a launch (blockIdx % 8: one XCD each under round-robin placement)
 constexpr int TEAM_MAX = 16;       // teams per launch: up to two per slot (TeamArgs::sub)
 constexpr int TEAM_MAXOPS = 24;    // operations per raster step
+constexpr int TEAM_TS_WORDS = 1024;   // stamp words per team (TeamArgs::ts)
 constexpr int TEAM_NI_MAX = 10;    // output tiles per workgroup and GEMM on the team kernel's fast path (64 images per
                                    // team: the context net's N = 1,152 layer deals 9 to a workgroup)
 struct TeamArgs {
@@ -124,8 +125,8 @@ struct TeamArgs {
     int split_op, split_wy;  // split_op >= 0: the GEMM after the rANS decode; its K slices w < split_wy (no y_qnt)
                              // run beside the rANS decode, the rest after it
     unsigned long long tmo;  // s_memrealtime ticks (100 MHz) one barrier waits before the launch gives up
-    unsigned long long* ts;  // optional [T][256]: s_memrealtime after every barrier of raster step (sv, sh), then
-                             // [64 + 8 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
+    unsigned long long* ts;  // optional [T][TEAM_TS_WORDS]: s_memrealtime after every barrier of raster step (sv, sh), then
+                             // [256 + 32 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
     int sv, sh;
     int dense;               // 1: the streams average >= 1 bit per symbol (high rates): every workgroup stages the
                              // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>

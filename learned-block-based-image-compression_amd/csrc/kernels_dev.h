@@ -154,7 +154,9 @@ struct BlkSrc {
 // Output element (row, col) of a GEMM from its slice-ordered sum v: bias + the layer's epilogue.  Shared by
 // both GEMM kernels so that they compute bit-identical values.
 // bcol = bias[col]; xv = the GDN input x[row][col] (GDN / IGDN only), both loaded by the caller.
-template <bool SC1 = false>
+// DEC: only the decoder's epilogues (the team kernel's instance: EPI_QUANT and EPI_SCATTER compiled out, so the code
+// every raster-step operation runs stays small -- the host records decoder GEMMs only and checks it)
+template <bool SC1 = false, bool DEC = false>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, int col, const BlkSrc& blocks, float bcol,
                                          float xv, bool wt = true) {
     switch (g.epi) {
@@ -203,6 +205,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             break;
         }
         case EPI_QUANT: {
+            if constexpr (DEC) break;
             const float y = v + bcol;
             const float scale = g.ksi[(long)row * g.ldk + col];
             const float mean = g.ksi[(long)row * g.ldk + g.Mlat + col];
@@ -228,6 +231,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, float v, int row, in
             break;
         }
         case EPI_SCATTER: {   // output row of block (img, v, h) -> out[img][v][h][col] (forward()'s xhat)
+            if constexpr (DEC) break;
             const int4 b = blocks.at(row);
             st<SC1>(g.out + ((long)b.x * g.HW + (long)b.y * g.geo.Wb + b.z) * g.ldo + col, v + bcol, wt);
             break;

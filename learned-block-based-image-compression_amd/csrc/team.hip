@@ -115,7 +115,7 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
 #pragma unroll
             for (int i = 1; i < KSPLIT; ++i) vv += rb[i * 256 + e];
             const int row = mt * 16 + (el >> 4) * 4 + er, col = nt * 16 + (el & 15);
-            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb, xx, wt);
+            if (row < g.M && col < g.N) epilogue<true, true>(g, vv, row, col, blocks, bb, xx, wt);
         }
     }
 }
@@ -131,11 +131,11 @@ __device__ __forceinline__ void team_gemm_long(const GemmArgs& g, int v, int h, 
 // their chains and leave the partials in LDS; 2 the remaining waves, then the reduction.
 // dts (sampled raster step, team rank 0; LBIC_TEAM_DIAG builds): wave 0's s_memtime at entry, loads issued, first
 // chain done, all chains done, outputs written.
-__device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep) {
+__device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep, bool every_wave = false) {
 #ifndef LBIC_TEAM_DIAG
-    (void)dts; (void)p; (void)dep;      // diagnostic build only (make team_diag): keeps the item loop's registers free
+    (void)dts; (void)p; (void)dep; (void)every_wave;   // diagnostic build only (make team_diag)
 #else
-    if (dts && threadIdx.x == 0) {
+    if (dts && (every_wave ? (threadIdx.x & 63) == 0 : threadIdx.x == 0)) {
         unsigned long long t;
         float d;       // the v_mov reads `dep` (an MFMA result): the stamp follows its chain
         asm volatile("v_mov_b32 %1, %2\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=v"(d) : "v"(dep) : "memory");
@@ -144,11 +144,9 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 #endif
 }
 
-template <int L, bool EXACT, bool SQ>
+template <int L, bool EXACT>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
                                                 float* red, bool wt, int ph, int wy, unsigned long long* dts) {
-    constexpr int LL = EXACT ? L : L + 1;
-    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
     constexpr int NPRE = 3;                      // output elements per thread (ni * 256 over 512 threads) whose epilogue
                                                  // operands are requested before the chains: every one up to 6 tiles
     const int lane = threadIdx.x & 63;
@@ -162,6 +160,9 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
     const int nout = ni * 256;
+    constexpr int LL = EXACT ? L : L + 1;
+    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
+    f4 a[LL], w0[LL], w1[LL];
     dstamp(dts, 0, 0.f);
     float bb[NPRE], xx[NPRE];
     if (ph != 1) {
@@ -177,7 +178,6 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     }
     dstamp(dts, 5, 0.f);
     if (act) {      // loads and chains in one branch: no join between a load and its use
-        f4 a[LL], w0[LL], w1[LL];
         auto issue = [&](int j, f4 (&w)[LL]) {
             const int nt = nt0 + (rank + j * S) / MT;
 #pragma unroll
@@ -188,11 +188,12 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             f4 acc = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < LL; ++c) {
-                f4 av = a[c];
-                if constexpr (SQ) av = av * av;     // GDN: squared A (a compile-time choice: no select, no temporaries)
+                const f4 av = a[c];
                 f4 t = acc;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], w[c][e], t, 0, 0, 0);
+                // (a select on every k-block, not only the (L+1)-th: the chain with a VALU select and its wait states
+                // between k-blocks runs faster than a back-to-back dependent MFMA chain -- measured, r06 call 5)
                 acc = c < n ? t : acc;
             }
             // partials -> LDS [item][slice][256]
@@ -200,6 +201,8 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             for (int i = 0; i < 4; ++i) red[(j * KSPLIT + wave) * 256 + i * 64 + lane] = acc[i];
             if (j == 0) dstamp(dts, 2, acc[0]);
             if (j == ni - 1) dstamp(dts, 3, acc[0]);
+            if (j == 0) dstamp(dts, 24 + wave, acc[0], true);
+            if (j == ni - 1) dstamp(dts, 16 + wave, acc[0], true);
         };
         issue(0, w0);
         dstamp(dts, 6, 0.f);
@@ -212,18 +215,29 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
         }
         dstamp(dts, 1, 0.f);
-        // the next item's fragments are requested unconditionally (the last request repeats the last item: an L2
-        // hit) so that no load sits behind a branch
+        // GDN (g.square_a): A squared once, in place, for every item (the same f32 products the chains used to form per
+        // item; a runtime choice, so one instance per slice length serves GDN and plain GEMMs -- fewer instances, less
+        // code for a raster step to fetch).  The next item's fragments are requested first, unconditionally (the last
+        // request repeats the last item: an L2 hit) so that no load sits behind a branch
+        auto square = [&]() {
+            if (g.square_a) {
+#pragma unroll
+                for (int c = 0; c < LL; ++c) a[c] = a[c] * a[c];
+            }
+        };
         if constexpr (PF) {
+            issue(min(1, ni - 1), w1);
+            square();
             for (int j = 0;;) {
-                issue(min(j + 1, ni - 1), w1);
                 chain(j, w0);
                 if (++j >= ni) break;
                 issue(min(j + 1, ni - 1), w0);
                 chain(j, w1);
                 if (++j >= ni) break;
+                issue(min(j + 1, ni - 1), w1);
             }
         } else {
+            square();
             for (int j = 0;;) {
                 chain(j, w0);
                 if (++j >= ni) break;
@@ -232,26 +246,37 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         }
     }
     if (ph == 1) return;
+    // the second round's epilogue operands (more than six tiles per workgroup) requested before the workgroup barrier:
+    // their latency hides behind the wait for the other waves' chains
+    static_assert(TEAM_NI_MAX * 256 <= 2 * NPRE * 512, "at most two epilogue rounds");
+    float bb1[NPRE], xx1[NPRE];
+    if ((int)threadIdx.x + 512 * NPRE < nout) {
+#pragma unroll
+        for (int q = 0; q < NPRE; ++q) {
+            const int o = min((int)threadIdx.x + 512 * (NPRE + q), nout - 1);
+            const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
+            const int nt = nt0 + (rank + j * S) / MT;
+            const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
+            bb1[q] = g.bias[ecol];
+            xx1[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+        }
+    }
     wg_bar();
+    dstamp(dts, 8, 0.f);
     // output o = threadIdx.x + 512 (NPRE r + q), round r: item j = o >> 8; its K slices' partials summed in slice order,
-    // then the epilogue.  Round 0's operands came before the chains; a further round (more than six tiles: 64 images
-    // per team, the context net's wide layers) loads its own into the same registers (a rolled loop: the epilogue's
-    // NPRE inlined copies serve every round)
+    // then the epilogue.  Round 0's operands came before the chains, round 1's before the barrier.  Both loops rolled:
+    // one copy of the (decoder-only) epilogue serves every output of an instance
 #pragma unroll 1
     for (int r = 0; (int)threadIdx.x + 512 * NPRE * r < nout; ++r) {
         if (r > 0) {
 #pragma unroll
             for (int q = 0; q < NPRE; ++q) {
-                const int o = min((int)threadIdx.x + 512 * (NPRE * r + q), nout - 1);
-                const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
-                const int nt = nt0 + (rank + j * S) / MT;
-                const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
-                bb[q] = g.bias[ecol];
-                xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
+                bb[q] = bb1[q];
+                xx[q] = xx1[q];
             }
         }
-#pragma unroll
-        for (int q = 0; q < NPRE; ++q) {
+#pragma unroll 1
+        for (int q = 0; q < NPRE; ++q) {      // rolled: one copy of the epilogue per instance
             const int o = threadIdx.x + 512 * (NPRE * r + q);
             if (o >= nout) break;
             const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
@@ -260,8 +285,11 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
             const int nt = nt0 + (rank + j * S) / MT;
             const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
-            if (row < g.M && col < g.N) epilogue<true>(g, vv, row, col, blocks, bb[q], xx[q], wt);
+            const float b_ = q == 0 ? bb[0] : q == 1 ? bb[1] : bb[2];
+            const float x_ = q == 0 ? xx[0] : q == 1 ? xx[1] : xx[2];
+            if (row < g.M && col < g.N) epilogue<true, true>(g, vv, row, col, blocks, b_, x_, wt);
         }
+        if (r == 0) dstamp(dts, 9, 0.f);
     }
     dstamp(dts, 4, 0.f);
 }
@@ -278,14 +306,12 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     if (ni == 0) return;
     if (team_fast_path(g, S)) {
         switch (L * 2 + (exact ? 1 : 0)) {
-#define LBIC_N(L_)                                                                                          \
-    case L_ * 2 + 1:                                                                                        \
-        if (g.square_a) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
-        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);          \
-        return;                                                                                             \
-    case L_ * 2:                                                                                            \
-        if (g.square_a) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts); \
-        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);         \
+#define LBIC_N(L_)                                                                            \
+    case L_ * 2 + 1:                                                                          \
+        team_gemm_items<L_, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);          \
+        return;                                                                               \
+    case L_ * 2:                                                                              \
+        team_gemm_items<L_, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);         \
         return;
             LBIC_N(1) LBIC_N(2) LBIC_N(3) LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
@@ -401,8 +427,8 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     typedef const __attribute__((address_space(4))) GemmArgs* cgemm_p;
     const cgemm_p G = (cgemm_p)(ta.gemm) + (long)team * 3 * ta.NG;
     const RansArgs& R = *(const RansArgs*)((crans_p)(ta.rans) + team);
-    unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * 256 : nullptr;
-    unsigned long long* tsr = ta.ts ? ta.ts + team * 256 : nullptr;   // every rank: [160 + rank] rANS done, [192 + rank]
+    unsigned long long* ts = ta.ts && rank == 0 ? ta.ts + team * TEAM_TS_WORDS : nullptr;
+    unsigned long long* tsr = ta.ts ? ta.ts + team * TEAM_TS_WORDS : nullptr;   // every rank: [160 + rank] rANS done, [192 + rank]
                                                                        // the GEMM waves beside it done (sampled step)
     if (ts && threadIdx.x == 0) ts[62] = __builtin_amdgcn_s_memrealtime();
     if constexpr (DENSE) {     // the rANS tables, once per launch (read-only: no hand-off)
@@ -438,7 +464,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                 if (k >= 0) {
                     const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + k);
                     team_gemm_any(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
-                                  samp ? ts + 64 + op * 8 : nullptr);
+                                  samp ? ts + 256 + op * 32 : nullptr);
                 } else {
                     // the rANS decode on the last nrw waves (wave i: rows rank + i S, rank + (i + nrw) S, ...); beside
                     // it the first split_wy <= KSPLIT - nrw waves compute the K slices of the next GEMM (the decoder's
