@@ -751,7 +751,9 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = world * n * H * W / (dt / args.steps) / 1e6
 
-    roof, kernels = roofline(kstats, dt, team_acc if args.team else None, enc_acc if args.team else None, args.steps)
+    headline_shape = (args.config, H, W, n) == ("B8_lowrate", 768, 768, 32)
+    roof, kernels = roofline(kstats, dt, team_acc if args.team else None, enc_acc if args.team else None, args.steps,
+                             cfg_key=None if headline_shape else args.config)
     mac_enc, mac_dec = arch.live_macs_per_block()
     step_flops = 2.0 * (mac_enc + mac_dec) * Hb * Wb * n
     cpu = None
@@ -836,7 +838,7 @@ def gather_records(rec, ok, dist):
     return torch.cat(allrec), bool(flag.item() == 1.0)
 
 
-def roofline(kstats, dt, team=None, enc=None, steps=0):
+def roofline(kstats, dt, team=None, enc=None, steps=0, cfg_key=None):
     """Dominant kernel family against its roofline.  Dominance = wall occupancy in the timed region, i.e. the time
     during which the family has a launch running, overlap with OTHER families allowed but never counted twice within
     one family: for the team decoder the summed durations of its launches (one at a time, HIP events around each), for
@@ -924,7 +926,8 @@ def roofline(kstats, dt, team=None, enc=None, steps=0):
             traffic_db = json.load(fh)
 
     def traffic_of(name):
-        pm = traffic_db.get(name, {})
+        # counters taken at this configuration's own launch shapes (tools/pmc_configs.sh) when it is not the headline's
+        pm = traffic_db.get("configs", {}).get(cfg_key, {}).get(name, {}) if cfg_key else traffic_db.get(name, {})
         if name == "k_dec_team" and team and "hbm_bytes_per_batch_step" in pm:
             # (counters at the headline's team shape; team["steps"] counts 32-frame batch raster steps)
             return round(pm["hbm_bytes_per_batch_step"] * team["steps"] / team["launches"]), pm.get("source")

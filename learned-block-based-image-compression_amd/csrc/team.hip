@@ -144,44 +144,63 @@ __device__ __forceinline__ void dstamp(unsigned long long* dts, int p, float dep
 #endif
 }
 
-template <int L, bool EXACT>
+// Buffer resource of a read-only or hand-off operand: 32-bit byte offsets (host-checked: < 4 GB)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t team_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
+}
+
+// ONESEG: A is one segment (every decoder GEMM but the two whose K spans the z-taps): its k-blocks are plain offsets
+// from one per-lane row address (a scalar offset per k-block), no per-k-block segment selection.  The prologue of an
+// operation -- epilogue operands, weight and A addressing -- is kept to scalar arithmetic and a few vector
+// instructions: it is issue-bound (the two waves of a SIMD run it one after the other before their chains start), so
+// every instruction there delays the slower wave of each SIMD and, through the workgroup barrier, the whole operation.
+template <int L, bool EXACT, bool ONESEG>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
                                                 float* red, bool wt, int ph, int wy, unsigned long long* dts) {
     constexpr int NPRE = 3;                      // output elements per thread (ni * 256 over 512 threads) whose epilogue
                                                  // operands are requested before the chains: every one up to 6 tiles
+    constexpr int LL = EXACT ? L : L + 1;
+    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nkb = g.K >> 4;
     const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
     const int MT = (g.M + 15) >> 4;
-    const int mt = rank % MT;
+    // (S % MT == 0 on the fast path) item j of this workgroup: row tile mt, column tile ntb + j nts
+    const int mt = rank % MT, ntb = nt0 + rank / MT, nts = S / MT;
     const BlkSrc blocks{nullptr, 1, 0, v, h};
     const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
-    const f4* Wt = reinterpret_cast<const f4*>(g.W) + lane;
     const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
     const int nout = ni * 256;
-    constexpr int LL = EXACT ? L : L + 1;
-    constexpr bool PF = LL <= 7;                 // prefetch the next item's fragments (128-VGPR budget)
+    // this thread's output elements o = threadIdx.x + 512 q: item j = (threadIdx.x >> 8) + 2 q, one row for all q
+    const int ol = threadIdx.x & 63, orr = (threadIdx.x >> 6) & 3, jt = threadIdx.x >> 8;
+    const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1);
+    const float* gxr = g.gx + (long)erow * g.ldx;
+    auto operands = [&](int q0, float (&b)[NPRE], float (&x)[NPRE]) {
+#pragma unroll
+        for (int q = 0; q < NPRE; ++q) {
+            const int j = min(jt + 2 * (q0 + q), ni - 1);     // clamped: every thread loads NPRE
+            const int ecol = min((ntb + j * nts) * 16 + (ol & 15), g.N - 1);
+            b[q] = g.bias[ecol];
+            x[q] = gdn ? ld<true>(gxr + ecol) : 0.f;
+        }
+    };
     f4 a[LL], w0[LL], w1[LL];
     dstamp(dts, 0, 0.f);
     float bb[NPRE], xx[NPRE];
-    if (ph != 1) {
-#pragma unroll
-        for (int q = 0; q < NPRE; ++q) {         // epilogue operands of output o = threadIdx.x + 512 q (item o >> 8),
-            const int o = min((int)threadIdx.x + 512 * q, nout - 1);    // clamped: every thread loads NPRE
-            const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
-            const int nt = nt0 + (rank + j * S) / MT;
-            const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
-            bb[q] = g.bias[ecol];
-            xx[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
-        }
-    }
+    if (ph != 1) operands(0, bb, xx);
     dstamp(dts, 5, 0.f);
     if (act) {      // loads and chains in one branch: no join between a load and its use
+        // weights: one buffer resource, this lane's 16 bytes of a fragment at lane * 16, the fragment's start in the
+        // scalar offset ((k-block * NB16 + column tile) KB)
+        const __amdgpu_buffer_rsrc_t wr = team_rsrc(g.W);
+        const unsigned lo16 = (unsigned)lane << 4;
         auto issue = [&](int j, f4 (&w)[LL]) {
-            const int nt = nt0 + (rank + j * S) / MT;
+            const int nt = ntb + j * nts;
 #pragma unroll
-            for (int c = 0; c < LL; ++c) w[c] = Wt[((long)min(kb0 + c, nkb - 1) * g.NB16 + nt) * 64];
+            for (int c = 0; c < LL; ++c)
+                w[c] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  wr, lo16, (unsigned)(min(kb0 + c, nkb - 1) * g.NB16 + nt) << 10, 0));
         };
         auto chain = [&](int j, f4 (&w)[LL]) {
             __builtin_amdgcn_sched_barrier(0);   // the requests above this item's chain
@@ -208,11 +227,24 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         dstamp(dts, 6, 0.f);
         {
             const SBlk bk = small_blk<true>(g, mt * 16, lane, blocks);
-            SRow rw;
-            small_offsets(g, bk, lane, rw);
-            dstamp(dts, 7, 0.f);
+            if constexpr (ONESEG) {
+                // this lane's row of the single segment; k-block kb at + kb * 64 bytes (scalar offset)
+                const Seg& sg = g.seg[0];
+                const long cell = ((long)bk.b.x * g.geo.Hp + bk.b.y + 2 + bk.dy) * g.geo.Wp + bk.b.z + 2 + bk.dx;
+                const unsigned ro = (unsigned)(((long)bk.r * sg.ld + sg.zs * cell + sg.tap + ((lane >> 4) << 2)) << 2);
+                const __amdgpu_buffer_rsrc_t ar = team_rsrc(sg.base);
+                dstamp(dts, 7, 0.f);
 #pragma unroll
-            for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
+                for (int c = 0; c < LL; ++c)
+                    a[c] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      ar, ro, (unsigned)min(kb0 + c, nkb - 1) << 6, 16));
+            } else {
+                SRow rw;
+                small_offsets(g, bk, lane, rw);
+                dstamp(dts, 7, 0.f);
+#pragma unroll
+                for (int c = 0; c < LL; ++c) a[c] = small_a_sc1(rw, min(kb0 + c, nkb - 1));
+            }
         }
         dstamp(dts, 1, 0.f);
         // GDN (g.square_a): A squared once, in place, for every item (the same f32 products the chains used to form per
@@ -250,22 +282,13 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     // their latency hides behind the wait for the other waves' chains
     static_assert(TEAM_NI_MAX * 256 <= 2 * NPRE * 512, "at most two epilogue rounds");
     float bb1[NPRE], xx1[NPRE];
-    if ((int)threadIdx.x + 512 * NPRE < nout) {
-#pragma unroll
-        for (int q = 0; q < NPRE; ++q) {
-            const int o = min((int)threadIdx.x + 512 * (NPRE + q), nout - 1);
-            const int j = o >> 8, ol = o & 63, orr = (o >> 6) & 3;
-            const int nt = nt0 + (rank + j * S) / MT;
-            const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1), ecol = min(nt * 16 + (ol & 15), g.N - 1);
-            bb1[q] = g.bias[ecol];
-            xx1[q] = gdn ? ld<true>(g.gx + (long)erow * g.ldx + ecol) : 0.f;
-        }
-    }
+    if ((int)threadIdx.x + 512 * NPRE < nout) operands(NPRE, bb1, xx1);
     wg_bar();
     dstamp(dts, 8, 0.f);
     // output o = threadIdx.x + 512 (NPRE r + q), round r: item j = o >> 8; its K slices' partials summed in slice order,
     // then the epilogue.  Round 0's operands came before the chains, round 1's before the barrier.  Both loops rolled:
     // one copy of the (decoder-only) epilogue serves every output of an instance
+    const int row = mt * 16 + (ol >> 4) * 4 + orr;
 #pragma unroll 1
     for (int r = 0; (int)threadIdx.x + 512 * NPRE * r < nout; ++r) {
         if (r > 0) {
@@ -279,12 +302,11 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
         for (int q = 0; q < NPRE; ++q) {      // rolled: one copy of the epilogue per instance
             const int o = threadIdx.x + 512 * (NPRE * r + q);
             if (o >= nout) break;
-            const int j = o >> 8, ee = o & 255, ol = o & 63, orr = (o >> 6) & 3;
+            const int j = o >> 8, ee = o & 255;
             float vv = red[j * KSPLIT * 256 + ee];
 #pragma unroll
             for (int i = 1; i < KSPLIT; ++i) vv += red[(j * KSPLIT + i) * 256 + ee];
-            const int nt = nt0 + (rank + j * S) / MT;
-            const int row = mt * 16 + (ol >> 4) * 4 + orr, col = nt * 16 + (ol & 15);
+            const int col = (ntb + j * nts) * 16 + (ol & 15);
             const float b_ = q == 0 ? bb[0] : q == 1 ? bb[1] : bb[2];
             const float x_ = q == 0 ? xx[0] : q == 1 ? xx[1] : xx[2];
             if (row < g.M && col < g.N) epilogue<true, true>(g, vv, row, col, blocks, b_, x_, wt);
@@ -306,12 +328,14 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
     if (ni == 0) return;
     if (team_fast_path(g, S)) {
         switch (L * 2 + (exact ? 1 : 0)) {
-#define LBIC_N(L_)                                                                            \
-    case L_ * 2 + 1:                                                                          \
-        team_gemm_items<L_, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);          \
-        return;                                                                               \
-    case L_ * 2:                                                                              \
-        team_gemm_items<L_, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);         \
+#define LBIC_N(L_)                                                                                            \
+    case L_ * 2 + 1:                                                                                          \
+        if (g.nseg == 1) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);   \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);              \
+        return;                                                                                               \
+    case L_ * 2:                                                                                              \
+        if (g.nseg == 1) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);  \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);             \
         return;
             LBIC_N(1) LBIC_N(2) LBIC_N(3) LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
