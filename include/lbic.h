@@ -177,9 +177,9 @@ int lbc_decode_team(lbc_model *const *ms, int n_teams, const uint8_t *const *str
 /* raw stamps of the last lbc_decode_team launch made with LBIC_TEAM_STAMPS=1, 1024 per team (team rank 0), s_memrealtime
  * (100 MHz): [op] after each barrier of the sampled raster step (Hb/2, Wb/2), [32 + op] when rank 0's own share of the
  * operation was done, [60] end of the step before it, [61] end of the sampled step, [62] launch start, [63] launch
- * end; s_memtime (shader clock) [256 + 32 op + p] inside the operation's GEMM (p: entry, A loads issued, first chain, all
+ * end; s_memtime (shader clock) [256 + 64 op + p] inside the operation's GEMM (p: entry, A loads issued, first chain, all
  * chains, outputs written, epilogue operands issued, first weights issued, offsets, partials reduced (8), first round
- * of outputs written (9), wave w's chains done (16 + w), its first chain done (24 + w)).  m = the call's first handle. */
+ * of outputs written (9), wave w's chains done (16 + w), its first chain done (24 + w), its A loads issued (32 + w), its first A fragment in (40 + w)).  m = the call's first handle. */
 int lbc_team_stamps(const lbc_model *m, unsigned long long *out, int max_out, int *n_out);
 /* the last lbc_decode_team launch led by m: its duration (HIP events around the launch), algorithmic bytes and FLOPs
  * (per raster step, the graph decoder's accounting: weights + A rows + outputs once per GEMM, rANS inputs and

@@ -1739,6 +1739,7 @@ static int team_record(lbc_model* const* ms, int T, int n_img, int Hb, int Wb, i
     // rANS waves per workgroup: two once the team has more images than workgroups (each wave then keeps one image's
     // coder state in LDS up to 2 S images; beyond that each wave decodes its rows one after another)
     a.nrw = n_img > S ? 2 : 1;
+    a.rows0 = n_img;
     // the GEMM after the rANS decode (the decoder's first layer): its last K segment is y_qnt; the K slices that end
     // before it run beside the rANS decode (on the waves the rANS decode leaves free) when every workgroup takes the
     // fast path for it

@@ -126,7 +126,7 @@ struct TeamArgs {
                              // run beside the rANS decode, the rest after it
     unsigned long long tmo;  // s_memrealtime ticks (100 MHz) one barrier waits before the launch gives up
     unsigned long long* ts;  // optional [T][TEAM_TS_WORDS]: s_memrealtime after every barrier of raster step (sv, sh), then
-                             // [256 + 32 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
+                             // [256 + 64 op + p] s_memtime inside its GEMMs (team_gemm_items, rank 0)
     int sv, sh;
     int dense;               // 1: the streams average >= 1 bit per symbol (high rates): every workgroup stages the
                              // rANS tables in its LDS once at launch start and the rANS operation runs rans_row<true>
@@ -138,6 +138,8 @@ struct TeamArgs {
                              // q S .. q S + S - 1 in launch order; spread = 1)
     int nrw;                 // rANS waves per workgroup (1 or 2: images per team up to S or 2 S decode side by side,
                              // wave i the rows rank + i S, rank + (i + nrw) S, ...)
+    int rows0;               // A rows of the step's usual GEMM (the images of a team): its row-tile quotients are
+                             // computed once per launch
 };
 // the team kernel's fast GEMM path (team_gemm_items) covers g for a team of S workgroups: what a split GEMM needs
 __host__ __device__ inline bool team_fast_path(const GemmArgs& g, int S) {

@@ -23,7 +23,11 @@ namespace lbic {
 // is multiplied, so a slice of K costs about one memory round trip instead of one per k-block.
 // OCC: minimum waves per SIMD the register allocation must allow (1 = no constraint).  The team decoder keeps
 // 256 of each SIMD's 512 VGPRs while it runs, so the encoder's residency beside it is (512 - 256) / its VGPRs.
-template <int BM, int BN, int NW, int CH, int OCC = 1>
+// ONE: A is a single dense segment (every layer but the first of each transform and of the context net): each
+// k-block's fragments are buffer loads at a per-lane row address plus a scalar k-block offset (weights likewise: lane *
+// 16 plus the fragment's scalar offset), with no per-k-block segment selection and no 64-bit address arithmetic -- the
+// k-loop issues its loads and MFMAs and little else (the encoder's GEMMs wait on instruction issue, round-3 PMC).
+template <int BM, int BN, int NW, int CH, int OCC = 1, bool ONE = false>
 __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
     constexpr int MS = BM / 16, NS = BN / 16, SPW = KSPLIT / NW;
     extern __shared__ __attribute__((aligned(16))) float red[];
@@ -66,6 +70,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
 
     const int nkb = g.K >> 4;
     const int nb0 = n0 >> 4;
+    // ONE: buffer resources of the A segment and the weights, per-lane byte addresses of this lane's A rows
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.seg[0].base), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.W), 0, -1, 0x00020000);
+    unsigned va[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) va[s] = (R.off[0][s] << 4) + (unsigned)(q4 << 2);
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
         const int slice = wave + q * NW;
@@ -76,7 +86,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void k_gemm(const GemmArgs g) {
         // skip their MFMAs, so the summation order is the plain k order for every CH
         auto load_chunk = [&](int base, Frag<MS, NS>(&f)[CH]) {
 #pragma unroll
-            for (int c = 0; c < CH; ++c) load_kb<MS, NS>(g, min(base + c, kb1 - 1), nb0, R, q4, lane, f[c]);
+            for (int c = 0; c < CH; ++c) {
+                const int kb = min(base + c, kb1 - 1);
+                if constexpr (ONE) {
+#pragma unroll
+                    for (int s = 0; s < MS; ++s)
+                        f[c].a[s] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, va[s], (unsigned)kb << 6, 0));
+#pragma unroll
+                    for (int j = 0; j < NS; ++j)
+                        f[c].w[j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                               rw, (unsigned)lane << 4, (unsigned)(kb * g.NB16 + nb0 + j) << 10, 0));
+                } else {
+                    load_kb<MS, NS>(g, kb, nb0, R, q4, lane, f[c]);
+                }
+            }
         };
         auto mma_chunk = [&](int base, Frag<MS, NS>(&f)[CH]) {
 #pragma unroll
@@ -240,7 +263,11 @@ constexpr int SMALL_MAX = 64, DEC_SMALL_MAX = 1024;
 // 0 = k_gemm_s (latency-shaped, any M; the decoder's raster steps stay on it when several batches are decoded
 // together: a raster step's latency barely grows with its rows), 1 = k_gemm (the encoder's wavefront steps)
 int gemm_class(const GemmArgs& g) {
-    return (g.M <= SMALL_MAX || (g.raster && g.M <= DEC_SMALL_MAX)) ? 0 : 1;
+    static const int small_max = [] {      // experiment hook: LBIC_ENC_SMALL = largest M on k_gemm_s
+        const char* e = getenv("LBIC_ENC_SMALL");
+        return e ? atoi(e) : SMALL_MAX;
+    }();
+    return (g.M <= small_max || (g.raster && g.M <= DEC_SMALL_MAX)) ? 0 : 1;
 }
 template <int BM, int BN, int NW, int CH, int OCC = 1>
 static int launch_cfg(const GemmArgs& g, hipStream_t s) {
@@ -249,11 +276,19 @@ static int launch_cfg(const GemmArgs& g, hipStream_t s) {
     static const bool attr = [] {     // once per instantiation (thread-safe static initialisation)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH, OCC>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<BM, BN, NW, CH, OCC, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, g);
+    // the single-dense-segment instance where its 32-bit buffer offsets reach every A row and weight fragment
+    const double a_end = ((double)(((g.M + BM - 1) / BM) * BM) * g.seg[0].ld + g.K) * 4.0;
+    const double w_end = (double)(g.K / 16) * g.NB16 * 1024.0;
+    if (g.nseg == 1 && g.seg[0].kind == SEG_DENSE && a_end < 4294967296.0 && w_end < 4294967296.0)
+        hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC, true>), grid, dim3(NW * 64), lds, s, g);
+    else
+        hipLaunchKernelGGL((k_gemm<BM, BN, NW, CH, OCC>), grid, dim3(NW * 64), lds, s, g);
     return launch_status("k_gemm");
 }
 

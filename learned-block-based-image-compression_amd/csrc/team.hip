@@ -156,7 +156,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t team_rsrc(const void* base) {
 // every instruction there delays the slower wave of each SIMD and, through the workgroup barrier, the whole operation.
 template <int L, bool EXACT, bool ONESEG>
 __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h, int rank, int S, int nt0, int ni,
-                                                float* red, bool wt, int ph, int wy, unsigned long long* dts) {
+                                                float* red, bool wt, int ph, int wy, unsigned long long* dts,
+                                                const int4& tq) {
     constexpr int NPRE = 3;                      // output elements per thread (ni * 256 over 512 threads) whose epilogue
                                                  // operands are requested before the chains: every one up to 6 tiles
     constexpr int LL = EXACT ? L : L + 1;
@@ -166,8 +167,12 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     const int nkb = g.K >> 4;
     const int kb0 = wave * nkb / KSPLIT, n = (wave + 1) * nkb / KSPLIT - kb0;
     const int MT = (g.M + 15) >> 4;
-    // (S % MT == 0 on the fast path) item j of this workgroup: row tile mt, column tile ntb + j nts
-    const int mt = rank % MT, ntb = nt0 + rank / MT, nts = S / MT;
+    // (S % MT == 0 on the fast path) item j of this workgroup: row tile mt, column tile ntb + j nts; the quotients
+    // precomputed once per launch for the step's usual row-tile count (tq: {MT, rank / MT, rank % MT, S / MT})
+    const bool pre = MT == tq.x;
+    const int mt = pre ? tq.z : (int)((unsigned)rank % (unsigned)MT);
+    const int ntb = nt0 + (pre ? tq.y : (int)((unsigned)rank / (unsigned)MT));
+    const int nts = pre ? tq.w : (int)((unsigned)S / (unsigned)MT);
     const BlkSrc blocks{nullptr, 1, 0, v, h};
     const bool gdn = g.epi == EPI_GDN || g.epi == EPI_IGDN;
     const bool act = ph == 0 || (ph == 1 ? wave < wy : wave >= wy);
@@ -175,14 +180,15 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
     // this thread's output elements o = threadIdx.x + 512 q: item j = (threadIdx.x >> 8) + 2 q, one row for all q
     const int ol = threadIdx.x & 63, orr = (threadIdx.x >> 6) & 3, jt = threadIdx.x >> 8;
     const int erow = min(mt * 16 + (ol >> 4) * 4 + orr, g.M - 1);
-    const float* gxr = g.gx + (long)erow * g.ldx;
+    // the GDN input row (other layers: the bias row again, read and not used): branch-free operand loads
+    const float* xr = gdn ? g.gx + (long)erow * g.ldx : g.bias;
     auto operands = [&](int q0, float (&b)[NPRE], float (&x)[NPRE]) {
 #pragma unroll
         for (int q = 0; q < NPRE; ++q) {
             const int j = min(jt + 2 * (q0 + q), ni - 1);     // clamped: every thread loads NPRE
             const int ecol = min((ntb + j * nts) * 16 + (ol & 15), g.N - 1);
             b[q] = g.bias[ecol];
-            x[q] = gdn ? ld<true>(gxr + ecol) : 0.f;
+            x[q] = ld<true>(xr + ecol);
         }
     };
     f4 a[LL], w0[LL], w1[LL];
@@ -247,6 +253,8 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
             }
         }
         dstamp(dts, 1, 0.f);
+        dstamp(dts, 32 + wave, 0.f, true);
+        dstamp(dts, 40 + wave, a[0][0], true);     // (waits for the first A fragment)
         // GDN (g.square_a): A squared once, in place, for every item (the same f32 products the chains used to form per
         // item; a runtime choice, so one instance per slice length serves GDN and plain GEMMs -- fewer instances, less
         // code for a raster step to fetch).  The next item's fragments are requested first, unconditionally (the last
@@ -318,7 +326,7 @@ __device__ __forceinline__ void team_gemm_items(const GemmArgs& g, int v, int h,
 
 // The output tiles of g this workgroup computes: rank `rank` of the team's S workgroups
 __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, int rank, int S, float* red, bool wt,
-                                              int ph, int wy, unsigned long long* dts) {
+                                              int ph, int wy, unsigned long long* dts, const int4& tq) {
     const int nt0 = 0, ntn = (g.N + 15) >> 4;
     const int nkb = g.K >> 4;
     const int L = nkb / KSPLIT;
@@ -330,12 +338,12 @@ __device__ __forceinline__ void team_gemm_any(const GemmArgs& g, int v, int h, i
         switch (L * 2 + (exact ? 1 : 0)) {
 #define LBIC_N(L_)                                                                                            \
     case L_ * 2 + 1:                                                                                          \
-        if (g.nseg == 1) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);   \
-        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);              \
+        if (g.nseg == 1) team_gemm_items<L_, true, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, tq);   \
+        else team_gemm_items<L_, true, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, tq);              \
         return;                                                                                               \
     case L_ * 2:                                                                                              \
-        if (g.nseg == 1) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);  \
-        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts);             \
+        if (g.nseg == 1) team_gemm_items<L_, false, true>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, tq);  \
+        else team_gemm_items<L_, false, false>(g, v, h, rank, S, nt0, ni, red, wt, ph, wy, dts, tq);             \
         return;
             LBIC_N(1) LBIC_N(2) LBIC_N(3) LBIC_N(4) LBIC_N(5) LBIC_N(6) LBIC_N(7) LBIC_N(8) LBIC_N(9)
 #undef LBIC_N
@@ -463,6 +471,13 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
     __syncthreads();
     unsigned target = 0;
     const bool wt = !ta.plain;
+    // the quotients of this rank by the usual row-tile count (the batch's images: ceil(M / 16) of every GEMM but the
+    // KS3311 context layer 0 at border columns), once per launch
+    int4 tq;
+    {
+        const unsigned mt0 = (unsigned)((ta.rows0 + 15) >> 4);
+        tq = make_int4((int)mt0, (int)((unsigned)rank / mt0), (int)((unsigned)rank % mt0), (int)((unsigned)S / mt0));
+    }
     if (ta.plain) {
         // placement census: every workgroup ORs its XCD into its team's word [1], then a barrier over the whole
         // grid (counter [T * 32 + 1]); any team on more than one XCD -> every workgroup leaves
@@ -488,7 +503,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                 if (k >= 0) {
                     const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + k);
                     team_gemm_any(g, v, h, rank, S, red, wt, op == ta.split_op ? 2 : 0, ta.split_wy,
-                                  samp ? ts + 256 + op * 32 : nullptr);
+                                  samp ? ts + 256 + op * 64 : nullptr, tq);
                 } else {
                     // the rANS decode on the last nrw waves (wave i: rows rank + i S, rank + (i + nrw) S, ...); beside
                     // it the first split_wy <= KSPLIT - nrw waves compute the K slices of the next GEMM (the decoder's
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(512, 4) void k_dec_team(const TeamArgs ta) {
                         if (sstep && lane == 0 && wave == rw0) tsr[160 + rank] = __builtin_amdgcn_s_memrealtime();
                     } else if (ta.split_op >= 0) {
                         const GemmArgs& g = *(const GemmArgs*)(G + cls * ta.NG + ta.opk[ta.split_op]);
-                        team_gemm_any(g, v, h, rank, S, red, wt, 1, ta.split_wy, nullptr);
+                        team_gemm_any(g, v, h, rank, S, red, wt, 1, ta.split_wy, nullptr, tq);
                         if (sstep && threadIdx.x == 0) tsr[192 + rank] = __builtin_amdgcn_s_memrealtime();
                     }
                 }

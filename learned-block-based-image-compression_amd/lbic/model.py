@@ -232,7 +232,7 @@ class BlockBasedImgCompLossyNetv9:
         """Raw stamps of the last decompress_teams launch led by this handle (LBIC_TEAM_STAMPS=1), [T, 256]
         (lbc_team_stamps, 256 per team): [op] after each barrier of the sampled raster step, [32 + op] rank 0's own
         work done, 60/61 the ends of the step before it and of the sampled step, 62/63 launch start / end (100 MHz);
-        [256 + 32 op + p] shader-clock stamps inside the operation's GEMM (1024 words per team)."""
+        [256 + 64 op + p] shader-clock stamps inside the operation's GEMM (1024 words per team)."""
         L = _lib.lib()
         n = ctypes.c_int(0)
         _lib.check(L.lbc_team_stamps(self._h, None, 0, ctypes.byref(n)))

@@ -107,8 +107,8 @@ def main():
                                             for k in range(32)],
                               gemm_beside_rans_done_us=[round((ts[0][192 + k] - ts[0][3]) / 100.0, 2) if ts[0][192 + k]
                                                         else None for k in range(32)],
-                              intra_cycles_team0=[[ts[0][256 + 32 * k + p] - ts[0][256 + 32 * k] if ts[0][256 + 32 * k + p] else 0
-                                                   for p in range(1, 32)] for k in range(12)])),
+                              intra_cycles_team0=[[ts[0][256 + 64 * k + p] - ts[0][256 + 64 * k] if ts[0][256 + 64 * k + p] else 0
+                                                   for p in range(1, 48)] for k in range(12)])),
               flush=True)
 
 
