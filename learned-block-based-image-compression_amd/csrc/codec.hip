@@ -1309,17 +1309,21 @@ int lbc_rans_decode_gpu(lbc_model* m, const uint8_t* const* streams, const size_
 // k_dec_one's program for this handle (one.hip): the raster step's 12 operations (context net x 4, rANS, decoder x 7,
 // exactly the layers, segments and epilogues run_ctx / run_dec give the graph decoder) and the placement of every weight
 // column tile in the LDS of one workgroup (greedy: each tile to the workgroup holding the fewest tiles of its GEMM, then
-// the least bytes).  Applies to KS[1] = 1 (no layer-0 cache), Mlat <= 256, K <= 1536 per GEMM, weights that fit the
-// grid's LDS; returns with m->one_ok = 0 otherwise.
+// the least bytes).  KS[1] = 3 runs the context net under the layer-0 cache as the graph decoder does (run_ctx, raster):
+// layer 0 computes its block's cell (and at a row end the border cell it owns) into the cache, layer 1 reads its five
+// 'B' taps as four cache cells and layer 0's granules; a column tile whose K x 16 weights exceed one workgroup's LDS
+// (B4_highrate's layer 1, K = 3,840) is held as two halves (OneOp::half).  Applies to Mlat <= 256, K slices of <= 11
+// k-blocks (<= 32 for a half-tile op), weights that fit the grid's LDS; returns with m->one_ok = 0 otherwise.
 static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     const std::vector<long long> key = {Hb, Wb, cus, m->net->gen, (long long)m->zpad.p, (long long)m->words.p,
                                         (long long)m->table_dev.p, (long long)m->st_x.p, (long long)m->cdf16_dev.p,
                                         (long long)m->tmeta_dev.p, (long long)m->word_base.p, (long long)m->st_status.p,
-                                        (long long)m->st_ptr.p, (long long)m->word_count.p};
+                                        (long long)m->st_ptr.p, (long long)m->word_count.p, (long long)m->l0.p};
     if (key == m->one_key) return LBC_OK;
     m->one_ok = 0;
     m->one_key = key;
-    if (m->l0_on || m->P != 1 || m->M > 256 || cus < 16) return LBC_OK;
+    if ((m->P != 1 && !m->l0_on) || m->M > 256 || cus < 16) return LBC_OK;
+    const bool l0 = m->l0_on;
     const Net& n = *m->net;
     std::vector<OneOp> ops(ONE_MAXOPS);
     auto gemm_op = [&](int o, const Layer& L, int epi, int sq) {
@@ -1343,7 +1347,17 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
             ops[o].seg[ops[o].nseg++] = OneSeg{ONE_ZTAP, -1, 0, TAPS_A[t][0], TAPS_A[t][1], t * m->Cx, (t + 1) * m->Cx};
     };
     gemm_op(0, n.ctx0, EPI_LEAKY, 0);  ztaps(0);                       // get_meanscale.0 ('A' 3x3 on the window)
-    gemm_op(1, n.ctx1, EPI_LEAKY, 0);  gran_seg(1, 0, 0, n.ctx1.K);
+    gemm_op(1, n.ctx1, EPI_LEAKY, 0);
+    if (l0) {       // layer 0 into the cache; layer 1 = the 3x3 'B' taps: four cache cells, then layer 0's own output
+        ops[0].l0out = 1;
+        for (int t = 0; t < 4; ++t)
+            ops[1].seg[ops[1].nseg++] = OneSeg{ONE_L0TAP, 0, 0, TAPS_B[t][0], TAPS_B[t][1], t * m->C1P, (t + 1) * m->C1P};
+        gran_seg(1, 0, 4 * m->C1P, 5 * m->C1P);
+        ops[1].l0seg = 1;
+        if (n.ctx1.K != 5 * m->C1P || n.ctx0.N != m->C1 || !m->l0.p) return LBC_OK;
+    } else {
+        gran_seg(1, 0, 0, n.ctx1.K);
+    }
     gemm_op(2, n.ctx2, EPI_LEAKY, 0);  gran_seg(2, 1, 0, n.ctx2.K);
     gemm_op(3, n.ctx3, EPI_CTXIDX, 0); gran_seg(3, 2, 0, n.ctx3.K);
     ops[4] = OneOp{};                                                 // the rANS decode: y_qnt granules
@@ -1358,12 +1372,31 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     gemm_op(10, n.ig2, EPI_IGDN, 1);   gran_seg(10, 9, 0, n.ig2.K); ops[10].gx_src = 9;
     gemm_op(11, n.d3, EPI_CLAMPZ, 0);  gran_seg(11, 10, 0, n.d3.K);
     if (n.d3.N != m->Cx || n.dec0.K != 4 * m->Cx + m->M || n.ctx0.K != 4 * m->Cx || n.ctx3.N != 2 * m->M) return LBC_OK;
-    // shape checks: K slices of 0..12 k-blocks, granule sources wide enough, segments contiguous
+    // weight capacity of one workgroup's LDS; a column tile larger than that, or with K slices past ONE_LL_MAX - 1
+    // k-blocks, is held as two halves (only layer-0 cache taps and granules as inputs there)
+    const size_t cap_f4 = (160 * 1024 - one_lds_bytes(0)) / 16;
+    for (int o = 0; o < ONE_MAXOPS; ++o) {
+        if (o == 4) continue;
+        const int nkb = ops[o].K / 16;
+        if ((size_t)nkb * 64 > cap_f4 || nkb / KSPLIT > ONE_LL_MAX - 1) {
+            bool ok = l0 && (nkb + KSPLIT - 1) / KSPLIT <= ONE_LLH_MAX && ops[o].epi == EPI_LEAKY && !ops[o].sq;
+            // (one_gemm_half: cache taps, then granules -- every cache segment before the first granule segment)
+            bool gran_seen = false;
+            for (int i = 0; i < ops[o].nseg; ++i) {
+                ok &= ops[o].seg[i].kind != ONE_ZTAP && !(gran_seen && ops[o].seg[i].kind == ONE_L0TAP);
+                gran_seen |= ops[o].seg[i].kind == ONE_GRAN;
+            }
+            if (!ok) return LBC_OK;
+            ops[o].half = 1;
+        }
+    }
+    // shape checks: K slices of 0..12 k-blocks (half-tile ops: 0..32), granule sources wide enough, segments contiguous
     for (int o = 0; o < ONE_MAXOPS; ++o) {
         const OneOp& q = ops[o];
         if (o == 4) continue;
         const int nkb = q.K / 16;
-        if (q.K % 16 || nkb < 1 || nkb / KSPLIT > ONE_LL_MAX - 1 || !q.W || !q.bias) return LBC_OK;
+        if (q.K % 16 || nkb < 1 || !q.W || !q.bias) return LBC_OK;
+        if (!q.half && nkb / KSPLIT > ONE_LL_MAX - 1) return LBC_OK;
         for (int i = 0; i < q.nseg; ++i) {
             const OneSeg& sg = q.seg[i];
             if ((sg.k0 & 15) || (i == 0 ? sg.k0 != 0 : sg.k0 != q.seg[i - 1].k1)) return LBC_OK;
@@ -1371,38 +1404,52 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
         }
         if (q.seg[q.nseg - 1].k1 != q.K) return LBC_OK;
     }
-    // granule buffers
+    // granule buffers (+ the half-tile ops' partials: two step parities x column tiles x 4 slices x 16)
     size_t ng = 0;
-    for (const OneOp& q : ops) ng += (size_t)q.gw;
+    for (const OneOp& q : ops) ng += (size_t)q.gw + (q.half ? (size_t)2 * q.gw * 4 : 0);
     int rc;
     if ((rc = m->one_gran.alloc(ng * 8))) return rc;
     size_t at = 0;
     for (OneOp& q : ops) {
         q.gran = m->one_gran.as<unsigned long long>() + at;
         at += (size_t)q.gw;
+        if (q.half) {
+            q.pgran = m->one_gran.as<unsigned long long>() + at;
+            at += (size_t)2 * q.gw * 4;
+        }
     }
-    // weight placement: workgroups 0 .. G - 2 hold tiles, G - 1 decodes the stream
+    // weight placement: workgroups 0 .. G - 2 hold tiles, G - 1 decodes the stream.  The half-tile pieces first (the
+    // largest), each to a workgroup that holds no other piece of a half-tile op (half 1 waits for half 0's partials
+    // inside the same operation: the two must run on different workgroups)
     const int G = cus;
-    const size_t cap_f4 = (160 * 1024 - one_lds_bytes(0)) / 16;
     std::vector<size_t> load(G, 0);
-    std::vector<int> held(G, 0);
+    std::vector<int> held(G, 0), has_half(G, 0);
     std::vector<int4> tiles((size_t)G * ONE_NT_MAX, make_int4(-1, 0, 0, 0));
-    for (int o = 0; o < ONE_MAXOPS; ++o) {
-        if (o == 4) continue;
+    std::vector<int> order;
+    for (int o = 0; o < ONE_MAXOPS; ++o)
+        if (o != 4 && ops[o].half) order.push_back(o);
+    for (int o = 0; o < ONE_MAXOPS; ++o)
+        if (o != 4 && !ops[o].half) order.push_back(o);
+    for (int o : order) {
         const int nt_n = (ops[o].N + 15) / 16;
-        const size_t sz = (size_t)(ops[o].K / 16) * 64;
+        const int nkb = ops[o].K / 16;
         std::vector<int> of_op(G, 0);
         for (int nt = 0; nt < nt_n; ++nt) {
-            int best = -1;
-            for (int g = 0; g < G - 1; ++g) {
-                if (held[g] >= ONE_NT_MAX || load[g] + sz > cap_f4) continue;
-                if (best < 0 || of_op[g] < of_op[best] || (of_op[g] == of_op[best] && load[g] < load[best])) best = g;
+            for (int pc = ops[o].half ? 1 : 0; pc <= (ops[o].half ? 2 : 0); ++pc) {
+                const int kb_lo = pc == 2 ? 4 * nkb / KSPLIT : 0, kb_hi = pc == 1 ? 4 * nkb / KSPLIT : nkb;
+                const size_t sz = (size_t)(kb_hi - kb_lo) * 64;
+                int best = -1;
+                for (int g = 0; g < G - 1; ++g) {
+                    if (held[g] >= ONE_NT_MAX || load[g] + sz > cap_f4 || (pc && has_half[g])) continue;
+                    if (best < 0 || of_op[g] < of_op[best] || (of_op[g] == of_op[best] && load[g] < load[best])) best = g;
+                }
+                if (best < 0) return LBC_OK;       // does not fit: the graph decoder keeps single images
+                tiles[(size_t)best * ONE_NT_MAX + held[best]] = make_int4(o, nt, (int)load[best], pc);
+                load[best] += sz;
+                held[best] += 1;
+                of_op[best] += 1;
+                has_half[best] |= pc ? 1 : 0;
             }
-            if (best < 0) return LBC_OK;       // does not fit: the graph decoder keeps single images
-            tiles[(size_t)best * ONE_NT_MAX + held[best]] = make_int4(o, nt, (int)load[best], 0);
-            load[best] += sz;
-            held[best] += 1;
-            of_op[best] += 1;
         }
     }
     size_t wmax = 0;
@@ -1428,6 +1475,8 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.Cx = m->Cx;
     a.Hb = Hb;
     a.Wb = Wb;
+    a.l0 = l0 ? m->l0.as<float>() : nullptr;
+    a.C1P = m->C1P;
     a.rans = m->one_rans.as<RansArgs>();
     a.Mlat = m->M;
     a.table = m->table_dev.as<float>();
@@ -1451,7 +1500,12 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     const char* e = getenv("LBIC_ONE");
     // (no_one: a team fallback after a residency timeout -- the chip's CUs are held elsewhere, and k_dec_one needs
     // every one of them co-resident, so it would likely time out again: go to the row graphs directly)
-    if ((e && atoi(e) == 0) || m->no_one || !rans_sparse_choice(lens, 1, (double)Hb * Wb * m->M)) return LBC_OK;
+    // k_dec_one decodes with the sparse rANS variant at any rate (its misses search the table image, copied into the
+    // rANS workgroup's LDS; bit-identical to the dense coder); LBIC_RANS_SPARSE=0 (the dense coder forced) keeps the
+    // row graphs
+    const char* rs = getenv("LBIC_RANS_SPARSE");
+    (void)lens;
+    if ((e && atoi(e) == 0) || m->no_one || (rs && atoi(rs) == 0)) return LBC_OK;
     int cus = 0, rc;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m->cfg.device));
     if ((rc = one_prepare(m, Hb, Wb, cus))) return rc;
@@ -1467,6 +1521,8 @@ static int decode_one(lbc_model* m, const size_t* lens, int Hb, int Wb, hipStrea
     }
     HIPCHK(hipMemsetAsync(m->one_gran.p, 0, m->one_gran.bytes, s));
     HIPCHK(hipMemsetAsync(m->one_fail.p, 0, 64, s));
+    // (KS[1] = 3) the layer-0 cache's row -1, as the graph decoder sets it: constant LeakyReLU(bias)
+    if (a.l0 && (rc = launch_l0_border(m->l0.as<float>(), 1, Hb, Wb, m->C1P, m->net->ctx0.bias.as<float>(), s))) return rc;
     if ((rc = launch_dec_one(a, m->one_grid, s))) return rc;
     if (a.ts) {
         m->one_ts_host.assign(ONE_TS_WORDS, 0ull);

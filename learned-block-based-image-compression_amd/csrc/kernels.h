@@ -156,30 +156,43 @@ constexpr int ONE_MAXOPS = 12;     // operations of a raster step: context net x
 constexpr int ONE_MAXSEG = 6;
 constexpr int ONE_NT_MAX = 4;      // weight tiles one workgroup holds
 constexpr int ONE_LL_MAX = 12;     // k-blocks of one K slice (K <= 1536)
-enum OneSrc : int { ONE_GRAN = 0, ONE_ZTAP = 1 };
+constexpr int ONE_LLH_MAX = 32;    // k-blocks of one K slice of a half-tile operation (OneOp::half: K <= 4096)
+enum OneSrc : int { ONE_GRAN = 0, ONE_ZTAP = 1, ONE_L0TAP = 2 };
 struct OneSeg {
     int kind;                // ONE_GRAN: columns [k0, k1) of K are columns [c0, c0 + k1 - k0) of op `src`'s granules;
-    int src, c0;             // ONE_ZTAP: the zpad tap (dy, dx) of the current block, channels [k - k0]
-    int dy, dx;
-    int k0, k1;
+    int src, c0;             // ONE_ZTAP: the zpad tap (dy, dx) of the current block, channels [k - k0];
+    int dy, dx;              // ONE_L0TAP (KS[1] = 3): the layer-0 cache cell (v + dy, h + dx), channels [k - k0],
+    int k0, k1;              //   ordered by op `src`'s granules (the cache's producer, the context net's layer 0)
 };
-struct OneOp {
+struct OneOp {             // (the epilogue's fields first: one scalar-cache line)
     const float* W;          // packed [K/16][NB16][4][16][4] (GEMMs; null for the rANS operation)
     const float* bias;
     int K, N, NB16, epi, sq; // epi: EPI_BIAS / EPI_LEAKY / EPI_IGDN / EPI_GDN / EPI_CTXIDX (value only) / EPI_CLAMPZ
-    int nseg;
-    OneSeg seg[ONE_MAXSEG];
-    int gx_src;              // GDN / IGDN: the op whose granules hold the layer input x
-    unsigned long long* gran;   // this op's output granules [gw] {float bits, step + 1}
+    int l0out;               // 1: the context net's layer 0 under the layer-0 cache (KS[1] = 3): every output also goes
+                             // to the cache cell of its position, and at a row end a second position (h = 0: (v, -1);
+                             // h = Wb - 1: (v - 1, Wb)) rides in MFMA row 1 (and 2 when Wb = 1) -- the graph decoder's
+                             // raster positions (codec.hip run_ctx)
+    int half;                // 1: every column tile is held as two halves (K slices 0-3 / 4-7) by two workgroups (a
+                             // whole tile would not fit one workgroup's LDS); half 0 hands its four slice partials over
+                             // as granules `pgran` [2 step parities][N / 16][4][16], half 1 sums all eight in slice order
     int gw;                  // granule width (N padded to 16)
+    unsigned long long* gran;   // this op's output granules [gw] {float bits, step + 1}
+    int l0seg;               // 1: layer-0 cache taps (ONE_L0TAP) among the segments
+    int nseg;
+    int gx_src;              // GDN / IGDN: the op whose granules hold the layer input x
+    OneSeg seg[ONE_MAXSEG];
+    unsigned long long* pgran;
 };
 struct OneArgs {
     const OneOp* ops;        // [nops] device, read-only for the launch
     int nops, rans_op, rans_wg;
-    const int4* tiles;       // [grid][ONE_NT_MAX] {op, column tile, LDS offset in float4s, 0}; op -1: none
+    const int4* tiles;       // [grid][ONE_NT_MAX] {op, column tile, LDS offset in float4s, piece}; op -1: none; piece
+                             // 0 the whole tile, 1 / 2 its half 0 / 1 (OneOp::half)
     int wlds_f4;             // float4s of weight tiles per workgroup (dynamic LDS)
     float* zpad;
     int Hp, Wp, Cx, Hb, Wb;
+    float* l0;               // the layer-0 map cache [Hb + 2][Wb + 4][C1P] (KS[1] = 3; zpad geometry), else null
+    int C1P;
     const RansArgs* rans;    // device: the stream's coder state / tables (idx, ksi, yq unused: LDS copies)
     int Mlat;
     const float* table;      // scale table (64)

@@ -12,7 +12,12 @@ decompress() (graphs/models/BlockBasedImgCompLossy_net.py:400-452) as eval_model
 * A launch whose waits time out (LBIC_ONE_TMO=1 tick) is decoded by the row graphs instead, counted, same result.
 * Truncated and corrupted streams decoded through k_dec_one raise (an overrun, or a decode that does not end in the
   encoder's initial rANS state), without a timeout, and the handle decodes correctly afterwards.
-* Geometries it does not cover (KS[1] = 3: the layer-0 cache; several images) keep the row graphs.
+* KS[1] = 3 (round 6): the context net under the layer-0 cache, B4_highrate's K = 3,840 layer 1 held as half tiles by
+  two workgroups, the high-rate streams through the sparse coder's table search -- the reference's own streams of the
+  KS3311 fixtures (tiny, B4_highrate at both operating points) and ragged B4 frames (one block column: three positions
+  in layer 0's MFMA at every step) decode through k_dec_one, equal the reference's decompress() and the row graphs bit
+  for bit; a damaged B4 stream raises.
+* Several images keep the row graphs; weights past the grid's LDS (B8_highrate, B16_lowrate) too.
 """
 import types
 
@@ -41,7 +46,8 @@ def _model(arch, seed, rate):
     return _M[key]
 
 
-@pytest.mark.parametrize("name", ["tiny_ks3111", "b8_lowrate_2rows", "b16_lowrate", "b16_lowrate_low"])
+@pytest.mark.parametrize("name", ["tiny_ks3111", "b8_lowrate_2rows", "b16_lowrate", "b16_lowrate_low", "tiny_ks3311",
+                                  "b4_highrate_mid", "b4_highrate", "b8_highrate_mid"])
 def test_one_decodes_reference_stream(name, monkeypatch):
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")       # k_dec_one decodes with the sparse rANS variant (any rate)
     g = load_golden("loop_" + name)
@@ -59,8 +65,9 @@ def test_one_decodes_reference_stream(name, monkeypatch):
     assert torch.equal(z1, zg), f"{name}: k_dec_one != row graphs ({(z1 != zg).sum().item()} values)"
     print(f"{name} (N{arch.N} B{arch.B}, {Hb}x{Wb} blocks): path {path['path']}, "
           f"max |zhat - zhat_dec(ref)| = {float(np.abs(z1[0].cpu().numpy() - ref).max()):.3e}")
-    if name in ("tiny_ks3111", "b8_lowrate_2rows"):
+    if name in ("tiny_ks3111", "b8_lowrate_2rows", "tiny_ks3311", "b4_highrate_mid", "b4_highrate"):
         assert path["path"] == "one", path
+        assert path["one_timeouts"] == 0, path
 
 
 @pytest.mark.parametrize("Hb,Wb", [(1, 7), (5, 1), (3, 2), (4, 9), (2, 96)])
@@ -75,6 +82,24 @@ def test_one_roundtrip_ragged(Hb, Wb):
     z = m.decompress_batch(st, Hb, Wb)
     assert m.decode_path()["path"] == "one"
     assert torch.equal(z, r["zhat"]), f"{Hb}x{Wb}: decode != encode"
+
+
+@pytest.mark.parametrize("Hb,Wb", [(1, 5), (4, 1), (3, 2), (3, 7)])
+def test_one_roundtrip_ragged_ks3311(Hb, Wb):
+    """B4_highrate (KS3311, layer-0 cache, half-tile layer 1) at its mid operating point: ragged frames -- one block row,
+    one block column (row ends on both sides at every step: three layer-0 positions), two columns -- decode through
+    k_dec_one to the encoder's reconstruction bit for bit."""
+    from lbic.arch import Arch
+    arch = Arch(4, (3, 3, 1, 1), 512, 96)
+    m = _model(arch, 1337, "mid")
+    x = torch.from_numpy(np.random.default_rng(Hb * 100 + Wb).integers(0, 256, (1, Hb, Wb, arch.cx))
+                         .astype(np.float32) / 255.0 - 0.5).cuda()
+    r = m.compress_batch(x)
+    st = m.entropy_encode(r["symbols"], r["indexes"])
+    z = m.decompress_batch(st, Hb, Wb)
+    p = m.decode_path()
+    assert p["path"] == "one" and p["one_timeouts"] == 0, p
+    assert torch.equal(z, r["zhat"]), f"{Hb}x{Wb}: decode != encode ({(z != r['zhat']).sum().item()} values)"
 
 
 def test_one_timeout_falls_back(monkeypatch):
@@ -97,15 +122,7 @@ def test_one_timeout_falls_back(monkeypatch):
     assert torch.equal(z, r["zhat"])
 
 
-def test_one_not_for_layer0_cache_or_batches():
-    g = load_golden("loop_tiny_ks3311")
-    arch = golden_arch(g)
-    m = _model(arch, int(g["weight_seed"]), golden_rate(g))
-    stream = O.GaussianTables().encode(g["symbols"], g["indexes"])
-    Hb, Wb = g["x"].shape[:2]
-    z = m.decompress_batch([stream], Hb, Wb)
-    assert m.decode_path()["path"] == "graphs"            # KS[1] = 3: the layer-0 cache is not in k_dec_one
-    assert_rel(z[0].cpu().numpy(), g["zhat_dec"])
+def test_one_not_for_batches():
     g = load_golden("loop_tiny_ks3111")
     arch = golden_arch(g)
     m = _model(arch, int(g["weight_seed"]), golden_rate(g))
@@ -117,11 +134,12 @@ def test_one_not_for_layer0_cache_or_batches():
 
 
 @pytest.mark.parametrize("damage", ["truncated", "corrupt_head", "corrupt_tail"])
-def test_one_bad_stream_raises(damage, monkeypatch):
+@pytest.mark.parametrize("name", ["tiny_ks3111", "b4_highrate_mid"])
+def test_one_bad_stream_raises(damage, name, monkeypatch):
     """A damaged stream through k_dec_one (sparse rANS forced, so the low-rate kernel runs whatever the stream's rate):
     the decode raises instead of returning a wrong image, no wait times out, and the handle still decodes."""
     monkeypatch.setenv("LBIC_RANS_SPARSE", "1")
-    g = load_golden("loop_tiny_ks3111")
+    g = load_golden("loop_" + name)
     arch = golden_arch(g)
     Hb, Wb = g["x"].shape[:2]
     stream = O.GaussianTables().encode(g["symbols"], g["indexes"])

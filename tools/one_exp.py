@@ -23,19 +23,29 @@ from lbic.weights import synth_state_dict  # noqa: E402
 OPS = ["ctx0", "ctx1", "ctx2", "ctx3", "rans", "dec0", "ig0", "d1", "ig1", "d2", "ig2", "d3", "rans_idx_coded"]
 
 
+CONFIGS = {   # name -> (B, KS, N, M, synthetic-weight operating point of the config: bench.py / lbic.weights)
+    "B8_lowrate": (8, (3, 1, 1, 1), 768, 96, "low"),
+    "B4_highrate": (4, (3, 3, 1, 1), 512, 96, "mid"),
+}
+
+
 def main():
+    # CONFIG: B8_lowrate (default) or B4_highrate (KS3311: layer-0 cache, half-tile layer 1); SIZE: frame side
+    B, KS, N, M, rate = CONFIGS[os.environ.get("CONFIG", "B8_lowrate")]
     size = int(os.environ.get("SIZE", "768"))
     reps = int(os.environ.get("REPS", "3"))
-    arch = Arch(8, (3, 1, 1, 1), 768, 96)
-    cfg = types.SimpleNamespace(block_size=8, KS=[3, 1, 1, 1], N=768, M=96, gpu_device=0)
+    arch = Arch(B, KS, N, M)
+    cfg = types.SimpleNamespace(block_size=B, KS=list(KS), N=N, M=M, gpu_device=0)
     m = BlockBasedImgCompLossyNetv9(cfg)
-    m.load_state_dict(synth_state_dict(arch, 1337, rate="low"))
+    m.load_state_dict(synth_state_dict(arch, 1337, rate=os.environ.get("RATE", rate)))
     m.update(force=True)
     img = np.random.default_rng(12345).integers(0, 256, (3, size, size), dtype=np.uint8).astype(np.float32) / 255 - 0.5
-    x = torch.from_numpy(image_to_blocks(img, 8))[None].cuda()
+    x = torch.from_numpy(image_to_blocks(img, B))[None].cuda()
     r = m.compress_batch(x)
     st = m.entropy_encode(r["symbols"], r["indexes"])
-    Hb = Wb = size // 8
+    print(json.dumps(dict(config=os.environ.get("CONFIG", "B8_lowrate"), bpp=len(st[0]) * 8.0 / (size * size))),
+          flush=True)
+    Hb = Wb = size // B
     for mode in ("1", "0"):
         os.environ["LBIC_ONE"] = mode
         ts = []
