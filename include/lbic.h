@@ -148,9 +148,10 @@ int lbc_rans_decode_gpu(lbc_model *m, const uint8_t *const *streams, const size_
 int lbc_decode(lbc_model *m, const uint8_t *const *streams, const size_t *lens, int n_img, int Hb, int Wb,
                float *zhat_dev, void *stream);
 /* How the last lbc_decode of this handle ran (no reference counterpart: a query for tests and the bench).  *path: 0
- * the row graphs (k_gemm_s / k_rans_decode chains), 1 the single-image decoder k_dec_one (n_img = 1 at low rates, KS[1]
- * = 1: one persistent launch over every CU, each weight tile resident in one workgroup's LDS, data-tagged hand-offs;
- * bit-identical to the row graphs; LBIC_ONE=0 disables it).  *timeouts: k_dec_one launches of this handle that timed out
+ * the row graphs (k_gemm_s / k_rans_decode chains), 1 the single-image decoder k_dec_one (n_img = 1 wherever the raster
+ * step's weights fit the grid's LDS -- B8_lowrate, B4_highrate with its KS[1] = 3 layer-0 cache -- at any rate: one
+ * persistent launch over every CU, each weight tile resident in one or two workgroups' LDS, data-tagged hand-offs;
+ * bit-identical to the row graphs; LBIC_ONE=0, or LBIC_RANS_SPARSE=0, disables it).  *timeouts: k_dec_one launches of this handle that timed out
  * waiting (CUs held elsewhere) and were decoded by the row graphs instead. */
 int lbc_decode_path(const lbc_model *m, int *path, int *timeouts);
 /* raw stamps of the last k_dec_one launch made with LBIC_ONE_STAMPS=1 (diagnostic): 4 per operation of the raster step

@@ -260,7 +260,8 @@ class BlockBasedImgCompLossyNetv9:
 
     def decode_path(self):
         """How the last decompress of this handle ran (lbc_decode_path): dict(path="graphs" | "one", one_timeouts) --
-        "one" = the single-image persistent decoder k_dec_one (one image, low rate, KS[1] = 1)."""
+        "one" = the single-image persistent decoder k_dec_one (one image whose step weights fit the grid's LDS:
+        B8_lowrate, B4_highrate)."""
         p, t = ctypes.c_int(), ctypes.c_int()
         _lib.check(_lib.lib().lbc_decode_path(self._h, ctypes.byref(p), ctypes.byref(t)))
         return dict(path=("graphs", "one")[p.value], one_timeouts=t.value)
