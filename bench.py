@@ -12,8 +12,8 @@ Schedule of the headline (`value`, `--team 16`, the default): one encoder handle
 own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the remainder) are decoded
 by ONE persistent k_dec_team launch (lbc_decode_team: one team of workgroups per 32-frame batch, two teams per XCD,
 team barriers instead of kernel boundaries) on a second stream, beside the encoder's next batches; the first launch
-takes part of every XCD's CUs (`--first-team-size`: 12 of 32 with up to 8 teams, 24 with 9-16), the rest left to the
-encoder.  `--team 0` selects the
+takes part of every XCD's CUs with up to 8 teams (`--first-team-size`: 12 of 32), every CU with 9-16 (the driver's 32
+batches: two launches of 16).  `--team 0` selects the
 `--workers` schedule (W codec handles on the shared weights, each compressing, entropy coding and decoding whole
 batches) or, with `--workers 0`, the encoder + `--depth` decoders pipeline.  The timed region holds exactly the `--steps` compressions and the `--steps`
 decompressions of the same batches, fill and drain included; inputs are resident in HBM when it starts.  Reported
@@ -95,12 +95,13 @@ def parse_args(argv=None):
                          "of two batches side by side, twice the row tiles per weight fetch; a launch then holds up to "
                          "2 x TEAM batches; 0 = auto: 2 for batches of at most 16 frames, else 1 -- the headline's "
                          "32-frame batches are decoded one per team)")
-    ap.add_argument("--first-team-size", type=int, default=12,
+    ap.add_argument("--first-team-size", type=int, default=-1,
                     help="team schedule: workgroups per XCD slot of each team in the FIRST decode launch, the one beside "
                          "the encoder's next batches (LBC_OPT_TEAM_SIZE; 0: all).  With up to 8 teams in that launch this "
                          "is the workgroups (CUs) per XCD, the rest left to the encoder; with 9-16 teams two teams share "
-                         "an XCD slot and each takes min(16, this), so 12 gives 24 of 32 (the bench line reports the "
-                         "actual count)")
+                         "an XCD slot and each takes min(16, this).  -1 (default): 12 with up to 8 teams (the driver's "
+                         "20 batches in round 5: 4 teams), every CU with 9-16 (32 batches: 16 teams, 120-123 vs 119-120 "
+                         "Mpix/s at 12, profiles/r06/fts_*)")
     ap.add_argument("--first-team-batches", type=int, default=0, choices=(0, 1, 2),
                     help="team schedule: batches per team in the FIRST decode launch (0: --team-batches)")
     ap.add_argument("--team-sizes", default="",
@@ -136,6 +137,10 @@ def parse_args(argv=None):
     ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
                     help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
                          "still decoded as its own 32-frame batch)")
+    ap.add_argument("--d2h-stream", type=int, default=1,
+                    help="team schedule, 1: the encoder's symbols / indexes go device -> host on a copy stream of their "
+                         "own (ordered after the compress by an event; the entropy coder waits for the copy), so the "
+                         "encoder stream starts the next batch at once; 0: on the encoder stream, synchronized")
     ap.add_argument("--per-image", type=int, default=1,
                     help="1: also time the reference's per-image path (eval_model, agents/blkbsdimgcomp_agent.py:591-599: "
                          "compress() then decompress() of ONE frame, batch 1), median of 3")
@@ -331,6 +336,9 @@ def main():
     # streams created before or between them, only the streams the team schedule uses, or another order moved the
     # encoder's and the decoder's hardware queues and cost up to 10 %: profiles/r03_exp/r03_q_*, r03_bench13_*)
     s_enc, = dedicated_streams(1, dev)
+    # (team schedule) the encoder's copy stream right after the encoder's: a hardware queue of its own, not one it would
+    # share with the busy team-decoder stream
+    s_d2h, = dedicated_streams(1, dev) if args.d2h_stream and args.team else (None,)
     s_decs = dedicated_streams(ndec, dev)
     enc_model = make_model()
     # decoder handles share the encoder handle's packed weights (one copy in the Infinity Cache)
@@ -374,14 +382,35 @@ def main():
         own moved 2-8 ms per batch off the encoder stream but gained 0.5 %, within noise: profiles/r03_exp.)"""
         model, stream = model or enc_model, stream or s_enc
         t0 = time.perf_counter()
-        with torch.cuda.stream(stream):
-            r = model.compress_batch(xb)
-            for k in ("symbols", "indexes"):
-                h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
-                h.copy_(r[k], non_blocking=True)
-                r[k] = h
-            stream.synchronize()
-        e_ms = model.last_timing()[0] if enc_acc["on"] else 0.0
+        if s_d2h is not None and stream is s_enc:
+            # the copies on their own stream: the encoder stream goes on with the next batch while they run; the device
+            # tensors are marked used by the copy stream (the allocator does not hand them out before the copy is
+            # done), and the entropy side waits for the copy's event
+            with torch.cuda.stream(stream):
+                r = model.compress_batch(xb)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            s_d2h.wait_event(ev)
+            with torch.cuda.stream(s_d2h):
+                for k in ("symbols", "indexes"):
+                    h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
+                    h.copy_(r[k], non_blocking=True)
+                    r[k].record_stream(s_d2h)
+                    r[k] = h
+                done = torch.cuda.Event()
+                done.record(s_d2h)
+            r["d2h_done"] = done
+            if not enc_acc["on"]:
+                stream.synchronize()      # (untimed / unprofiled passes: one batch at a time, as before)
+        else:
+            with torch.cuda.stream(stream):
+                r = model.compress_batch(xb)
+                for k in ("symbols", "indexes"):
+                    h = torch.empty(r[k].shape, dtype=r[k].dtype, pin_memory=True)
+                    h.copy_(r[k], non_blocking=True)
+                    r[k] = h
+                stream.synchronize()
+        e_ms = model.last_timing()[0] if enc_acc["on"] else 0.0     # (waits for this compress, not for its copy)
         with plock:
             ph["encode"] += time.perf_counter() - t0
             if enc_acc["on"]:
@@ -391,10 +420,12 @@ def main():
 
     def split_record(r, e):
         """Batch e (n frames) of a multi-batch compress record."""
-        return {kk: (v[e * n:(e + 1) * n] if v is not None else None) for kk, v in r.items()}
+        return {kk: (v if kk == "d2h_done" else v[e * n:(e + 1) * n] if v is not None else None) for kk, v in r.items()}
 
     def entropy_side(r, fmt, ph, model=None):
         t0 = time.perf_counter()
+        if r.get("d2h_done") is not None:
+            r["d2h_done"].synchronize()
         st = (model or enc_model).entropy_encode(r["symbols"], r["indexes"], fmt=fmt, Hb=Hb, Wb=Wb)
         with plock:
             ph["entropy"] += time.perf_counter() - t0
@@ -470,6 +501,11 @@ def main():
                                      args.team_sizes if args.team_sizes and steps == args.steps else "",
                                      args.first_team_batches if not tbatches else 0, len(dec_models))
 
+            def first_size(teams):
+                if args.first_team_size >= 0:
+                    return args.first_team_size
+                return 12 if teams <= 8 else 0
+
             def team_decoder():
                 pend = []
                 gi = 0
@@ -494,7 +530,7 @@ def main():
                                 # profiles/r02_exp/team_two_per_cu.txt)
                                 zt = decompress_teams(dec_models[:len(tsts)], tsts, Hb, Wb,
                                                       wg_per_cu=args.drain_wg_per_cu if last else 1,
-                                                      team_size=args.first_team_size if gi == 1 and not last else 0)
+                                                      team_size=first_size(len(tsts)) if gi == 1 and not last else 0)
                                 sd_.synchronize()
                             zs = [z_[e * n:(e + 1) * n] for z_ in zt for e in range(tb_)]
                             with plock:
@@ -764,6 +800,7 @@ def main():
     first_teams = 0
     if args.team and team_acc["windows"] and len(team_acc["windows"]) > 1:
         first_teams = team_acc["windows"][0][3]          # teams of the first launch (the one beside the encoder)
+    fts_used = args.first_team_size if args.first_team_size >= 0 else (12 if first_teams <= 8 else 0)
     out = {
         "metric": METRIC if (args.config, H, W) == ("B8_lowrate", 768, 768) else
         f"Mpixels/s encode+decode, {args.config} N{N}M{M}, {W}×{H}", "value": round(value, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
@@ -781,8 +818,9 @@ def main():
                                    f"team of workgroups ({n * tb_cfg} images per team side by side), up to {args.team} "
                                    "teams per launch")
                                   + (f"; the first launch (beside the encoder's next batches: {first_teams} teams) on "
-                                     f"{first_wg_per_xcd(first_teams, args.first_team_size)} of every busy XCD's 32 CUs"
-                                     if args.first_team_size and first_teams else "") if args.team else
+                                     + (f"{first_wg_per_xcd(first_teams, fts_used)} of every busy XCD's 32 CUs" if fts_used
+                                        else "every CU")
+                                     if first_teams else "") if args.team else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "
                                   f"up to {args.workers} passes in flight (one per worker)" if args.workers else
                                   f"each decode pass decodes one {n}-frame batch ({n} frames in flight per pass), "

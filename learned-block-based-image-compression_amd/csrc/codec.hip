@@ -1374,7 +1374,8 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     if (n.d3.N != m->Cx || n.dec0.K != 4 * m->Cx + m->M || n.ctx0.K != 4 * m->Cx || n.ctx3.N != 2 * m->M) return LBC_OK;
     // weight capacity of one workgroup's LDS; a column tile larger than that, or with K slices past ONE_LL_MAX - 1
     // k-blocks, is held as two halves (only layer-0 cache taps and granules as inputs there)
-    const size_t cap_f4 = (160 * 1024 - one_lds_bytes(0)) / 16;
+    const int red_rows = l0 ? 3 : 1;
+    const size_t cap_f4 = (160 * 1024 - one_lds_bytes(0, red_rows)) / 16;
     for (int o = 0; o < ONE_MAXOPS; ++o) {
         if (o == 4) continue;
         const int nkb = ops[o].K / 16;
@@ -1477,6 +1478,7 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.Wb = Wb;
     a.l0 = l0 ? m->l0.as<float>() : nullptr;
     a.C1P = m->C1P;
+    a.red_rows = red_rows;
     a.rans = m->one_rans.as<RansArgs>();
     a.Mlat = m->M;
     a.table = m->table_dev.as<float>();
@@ -1486,7 +1488,7 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.rans_lds_tab = (size_t)m->total16 * 2 <= wmax * 16 && m->total16 % 8 == 0 ? 1 : 0;
     a.ts_step = (Hb / 2) * Wb + Wb / 2;
     if ((rc = m->one_ts.alloc(ONE_TS_WORDS * sizeof(unsigned long long)))) return rc;
-    if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4)) < 1) return LBC_OK;
+    if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4, a.red_rows)) < 1) return LBC_OK;
     m->one_grid = G;
     m->one_ok = 1;
     return LBC_OK;

@@ -193,6 +193,7 @@ struct OneArgs {
     int Hp, Wp, Cx, Hb, Wb;
     float* l0;               // the layer-0 map cache [Hb + 2][Wb + 4][C1P] (KS[1] = 3; zpad geometry), else null
     int C1P;
+    int red_rows;            // MFMA rows of the partials area: 3 with the layer-0 cache (row-end positions), else 1
     const RansArgs* rans;    // device: the stream's coder state / tables (idx, ksi, yq unused: LDS copies)
     int Mlat;
     const float* table;      // scale table (64)
@@ -215,7 +216,7 @@ struct OneArgs {
 constexpr int ONE_TS_DETAIL = ONE_MAXOPS * 4 + 4;
 constexpr int ONE_TS_PER_OP = 32;
 constexpr int ONE_TS_WORDS = ONE_TS_DETAIL + ONE_MAXOPS * ONE_TS_PER_OP;
-size_t one_lds_bytes(int wlds_f4);
+size_t one_lds_bytes(int wlds_f4, int red_rows);
 int one_blocks_per_cu(size_t lds);
 int launch_dec_one(const OneArgs& a, int grid, hipStream_t s);
 

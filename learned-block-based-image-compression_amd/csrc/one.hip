@@ -599,11 +599,11 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
 
 }  // namespace
 
-// dynamic LDS: [weight tiles wlds_f4 float4s][partials 3 rows x KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
+// dynamic LDS: [weight tiles wlds_f4 float4s][partials red_rows (1; 3 under the layer-0 cache) x KSPLIT x 16][A scratch 8 x ONE_SCR][rANS window RANS_WIN words]
 // [rANS state cache ONE_RC_WORDS][scale indexes | means 512][yq 256][flag 4 words][stamp slots ONE_NT_MAX x ONE_TS_PER_OP
 // u64][scale table 64][rANS centre intervals 256]
-size_t one_lds_bytes(int wlds_f4) {
-    return (size_t)wlds_f4 * 16 + (size_t)(3 * KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
+size_t one_lds_bytes(int wlds_f4, int red_rows) {
+    return (size_t)wlds_f4 * 16 + (size_t)(red_rows * KSPLIT * 16 + KSPLIT * ONE_SCR) * 4 +
            (size_t)(RANS_WIN + ONE_RC_WORDS + 512 + 256 + 4) * 4 + (size_t)ONE_NT_MAX * ONE_TS_PER_OP * 8 + 64 * 4 +
            256 * 4;
 }
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t one_lds[];
     f4* wl = reinterpret_cast<f4*>(one_lds);
     float* red = reinterpret_cast<float*>(wl + a.wlds_f4);
-    float* scr = red + 3 * KSPLIT * 16;
+    float* scr = red + a.red_rows * KSPLIT * 16;
     uint32_t* lwin = reinterpret_cast<uint32_t*>(scr + KSPLIT * ONE_SCR);
     uint32_t* rcache = lwin + RANS_WIN;
     float* l_ksi = reinterpret_cast<float*>(rcache + ONE_RC_WORDS);
@@ -785,7 +785,8 @@ int launch_dec_one(const OneArgs& a, int grid, hipStream_t s) {
         a.rans_wg < 0 || a.rans_wg >= grid || a.rans_op < 1 || a.rans_op >= a.nops || a.Mlat > 256 || a.Mlat < 1 ||
         (a.l0 && a.C1P % 16))
         return set_error(LBC_E_ARG, "bad single-image decoder arguments");
-    const size_t lds = one_lds_bytes(a.wlds_f4);
+    if (a.red_rows != (a.l0 ? 3 : 1)) return set_error(LBC_E_ARG, "single-image decoder: partial rows");
+    const size_t lds = one_lds_bytes(a.wlds_f4, a.red_rows);
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "single-image decoder: LDS image too large");
     static const bool attr = [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_one), hipFuncAttributeMaxDynamicSharedMemorySize,
