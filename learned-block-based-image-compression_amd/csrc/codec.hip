@@ -1488,7 +1488,7 @@ static int one_prepare(lbc_model* m, int Hb, int Wb, int cus) {
     a.rans_lds_tab = (size_t)m->total16 * 2 <= wmax * 16 && m->total16 % 8 == 0 ? 1 : 0;
     a.ts_step = (Hb / 2) * Wb + Wb / 2;
     if ((rc = m->one_ts.alloc(ONE_TS_WORDS * sizeof(unsigned long long)))) return rc;
-    if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4, a.red_rows)) < 1) return LBC_OK;
+    if (one_blocks_per_cu(one_lds_bytes(a.wlds_f4, a.red_rows), l0) < 1) return LBC_OK;
     m->one_grid = G;
     m->one_ok = 1;
     return LBC_OK;

@@ -217,7 +217,7 @@ constexpr int ONE_TS_DETAIL = ONE_MAXOPS * 4 + 4;
 constexpr int ONE_TS_PER_OP = 32;
 constexpr int ONE_TS_WORDS = ONE_TS_DETAIL + ONE_MAXOPS * ONE_TS_PER_OP;
 size_t one_lds_bytes(int wlds_f4, int red_rows);
-int one_blocks_per_cu(size_t lds);
+int one_blocks_per_cu(size_t lds, bool l0);
 int launch_dec_one(const OneArgs& a, int grid, hipStream_t s);
 
 int prepare_gemm(GemmArgs& g);     // launch_gemm's host-side checks and segment set-up, without the launch

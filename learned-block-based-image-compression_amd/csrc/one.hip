@@ -568,21 +568,23 @@ __device__ __forceinline__ bool one_gemm_half(const OneArgs& a, const OneOp& op,
 
 // LL = fragments per wave: L = (K / 16) / 8 k-blocks per slice, L + 1 when the slices differ in length (the extra
 // fragment's MFMAs are discarded), L when every slice has exactly L (nothing to discard: a shorter chain)
+// KL0: the kernel instance under the layer-0 cache (k_dec_one<true>); the other instance compiles no cache code at all
+template <bool KL0>
 __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, int o, const int4 (&my)[ONE_NT_MAX], int v, int h,
                              unsigned tag, const f4* wl, float* red, float* scr, int* sflag, const OneCtl& c,
                              unsigned long long* lst, const float* ltab) {
     const int nkb = op.K >> 4;
-    const bool l0 = op.l0out || op.l0seg;
+    const bool l0 = KL0 && (op.l0out || op.l0seg);
     int key = (nkb / KSPLIT) * 2 + (nkb % KSPLIT == 0 ? 1 : 0);
 #ifndef LBIC_ONE_EXACT_ALL
     if ((key & 1) && key != 13 && key != 19) key &= ~1;     // exact slices without an instance: the L + 1 form
 #endif
     switch (key) {
 #define LBIC_ONE(L_) \
-    case L_ * 2: return l0 ? one_gemm<L_ + 1, true>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab) \
+    case L_ * 2: return l0 ? one_gemm<L_ + 1, KL0>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab) \
                            : one_gemm<L_ + 1, false>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
 #define LBIC_ONE_EX(L_) \
-    case L_ * 2 + 1: return l0 ? one_gemm<L_, true>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab) \
+    case L_ * 2 + 1: return l0 ? one_gemm<L_, KL0>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab) \
                                : one_gemm<L_, false>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
         LBIC_ONE(0) LBIC_ONE(1) LBIC_ONE(2) LBIC_ONE(3) LBIC_ONE(4) LBIC_ONE(5) LBIC_ONE(6) LBIC_ONE(7) LBIC_ONE(8)
         LBIC_ONE(9) LBIC_ONE(10) LBIC_ONE(11)
@@ -608,6 +610,8 @@ size_t one_lds_bytes(int wlds_f4, int red_rows) {
            256 * 4;
 }
 
+// L0: KS[1] = 3 (the layer-0 cache, half-tile operations); L0 = false is the KS[1] = 1 kernel without any of that code
+template <bool L0>
 __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t one_lds[];
     f4* wl = reinterpret_cast<f4*>(one_lds);
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
             for (int i = 0; i < ONE_NT_MAX; ++i) mine |= my[i].x == o;
             if (!mine) continue;
             const OneOp& op = *(const OneOp*)((cop_p)a.ops + o);
-            if (op.half) {     // (one piece of a half-tile op per workgroup: host-checked)
+            if (L0 && op.half) {     // (one piece of a half-tile op per workgroup: host-checked)
                 int sl = 0;
 #pragma unroll
                 for (int i = ONE_NT_MAX - 1; i >= 1; --i) sl = my[i].x == o ? i : sl;
@@ -729,7 +733,7 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
                 if (!good) return;
                 continue;
             }
-            if (!one_gemm_any(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab_s)) return;
+            if (!one_gemm_any<L0>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab_s)) return;
         }
     }
     // the stamps of step ts_step, from LDS to memory after the last step
@@ -770,13 +774,14 @@ __global__ __launch_bounds__(512, 1) void k_dec_one(const OneArgs a) {
     }
 }
 
-int one_blocks_per_cu(size_t lds) {
+static const void* one_instance(bool l0) {
+    return l0 ? reinterpret_cast<const void*>(&k_dec_one<true>) : reinterpret_cast<const void*>(&k_dec_one<false>);
+}
+
+int one_blocks_per_cu(size_t lds, bool l0) {
     int nb = 0;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_one), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_dec_one), 512, lds) !=
-        hipSuccess)
-        return 0;
+    (void)hipFuncSetAttribute(one_instance(l0), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, one_instance(l0), 512, lds) != hipSuccess) return 0;
     return nb;
 }
 
@@ -789,12 +794,13 @@ int launch_dec_one(const OneArgs& a, int grid, hipStream_t s) {
     const size_t lds = one_lds_bytes(a.wlds_f4, a.red_rows);
     if (lds > 160 * 1024) return set_error(LBC_E_ARG, "single-image decoder: LDS image too large");
     static const bool attr = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec_one), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        for (int l = 0; l < 2; ++l)
+            (void)hipFuncSetAttribute(one_instance(l != 0), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL(k_dec_one, dim3(grid), dim3(512), lds, s, a);
+    if (a.l0) hipLaunchKernelGGL(k_dec_one<true>, dim3(grid), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(k_dec_one<false>, dim3(grid), dim3(512), lds, s, a);
     return launch_status("k_dec_one");
 }
 
