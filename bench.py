@@ -5,8 +5,10 @@ Workload (BASELINE.json configs[1]): B8_lowrate (B=8, KS=3,1,1,1, N=768, M=96), 
 768x768 frames per GPU, in the reference bitstream format (one raster rANS stream per image).  One step =
 the reference's timed region of eval_model (agents/blkbsdimgcomp_agent.py:591-599) for one 32-frame batch:
 compress (GPU wavefront closed loop + host rANS encode) and decompress (GPU raster closed loop with GPU
-rANS decode).  Every batch is encoded as its own 32-frame wavefront pass and decoded as its own 32-frame raster pass
-(one team of workgroups per batch).
+rANS decode).  Four batches share one 128-frame encoder wavefront pass (`--enc-pass`; every launch of the encoder's
+GEMMs has four times the rows, its partly filled last round of workgroups amortised over more frames), and every batch
+is entropy coded and decoded as its own 32-frame raster pass (one team of workgroups per batch); the line reports the
+one-batch-per-pass schedule beside it (`one_batch_per_encode_pass`).
 
 Schedule of the headline (`value`, `--team 16`, the default): one encoder handle compresses batch after batch on its
 own HIP stream (host rANS on helper threads); every 16 encoded batches (the first group: the remainder) are decoded
@@ -134,9 +136,13 @@ def parse_args(argv=None):
                          "the same-command rocprof summary holds only the headline's kernel shapes)")
     ap.add_argument("--substream-steps", type=int, default=0, help="batches in the opt-in sub-stream format (0 = skip)")
     ap.add_argument("--encode-only", type=int, default=0, help="profiling aid: this many encoder passes, no JSON")
-    ap.add_argument("--enc-pass", type=int, default=1, choices=(1, 2),
-                    help="team schedule: batches per encoder pass (2: two 32-frame batches in one wavefront pass, each "
-                         "still decoded as its own 32-frame batch)")
+    ap.add_argument("--enc-pass", type=int, default=4, choices=(1, 2, 4),
+                    help="team schedule: batches per encoder pass (2, 4: that many 32-frame batches in one wavefront "
+                         "pass -- each launch of the encoder's GEMMs then has 2 / 4 times the rows, so its last, partly "
+                         "filled round of workgroups is amortised over more frames -- each batch still entropy coded and "
+                         "decoded as its own 32-frame batch; the driver's 32 batches, profiles/r06/exp/encpass_*: 1 / 2 / "
+                         "4 batches per pass 119.7-120.0 / 128.0-128.4 / 130.6-130.7 Mpix/s; the line reports the one-"
+                         "batch figure beside it, one_batch_per_encode_pass)")
     ap.add_argument("--d2h-stream", type=int, default=1,
                     help="team schedule, 1: the encoder's symbols / indexes go device -> host on a copy stream of their "
                          "own (ordered after the compress by an event; the entropy coder waits for the copy), so the "
@@ -351,7 +357,7 @@ def main():
 
     # two distinct 32-frame sets per rank (batch k codes set k % 2); the gang schedule's encoder passes
     # compress `gang` batches of distinct frames at once
-    nsets = max(2, args.gang)
+    nsets = max(2, args.gang, args.enc_pass if args.team else 1)
     frames = np.stack([image_to_blocks(np.random.default_rng(rank * n * nsets + k).integers(0, 256, (3, H, W),
                                                                                     dtype=np.uint8)
                                        .astype(np.float32) / 255.0 - 0.5, B) for k in range(n * nsets)])
@@ -359,7 +365,7 @@ def main():
     del frames
 
     def frames_of(k):
-        s = k % 2
+        s = k % (nsets if args.team and args.enc_pass > 2 else 2)
         return xb_all[s * n:(s + 1) * n]
 
     def barrier():
@@ -453,7 +459,8 @@ def main():
     team_acc = dict(launches=0, ms=0.0, bytes=0.0, flops=0.0, steps=0, plain=[], timeouts=0, windows=[], enc_done=0.0,
                     modes=[])
 
-    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0, tbatches=0):
+    def pipeline(steps, depth, fmt="reference", gang=1, prof=False, label="", base=0, workers=0, team=0, tbatches=0,
+                 enc_pass=0):
         """`steps` batches through the pipeline, all inside the timed region: this thread compresses batch k
         (or `gang` batches in one wavefront pass) while a helper thread entropy codes the previous one and
         `depth` decoder threads each decode `gang` queued batches per raster pass (their own handles and
@@ -562,15 +569,16 @@ def main():
             with ThreadPoolExecutor(max_workers=4) as ex:
                 k = 0
                 while k < steps:
-                    g = min(args.enc_pass, steps - k)
-                    if args.enc_pass == 1 or (base + k) % 2:
+                    P_ = enc_pass or args.enc_pass
+                    g = min(P_, steps - k)
+                    if P_ == 1 or (base + k) % P_:
                         g = 1
                         rs_ = [compress_side(ph, frames_of(base + k))]
                     else:
-                        # batches k, k + 1 = frame sets 0, 1 (contiguous in xb_all): one wavefront pass.  An odd last
-                        # batch is coded in a two-batch pass as well (its partner's codes are dropped): the encoder
-                        # graph keeps one frame count, so no pass re-captures it
-                        rr_ = compress_side(ph, xb_all[:2 * n])
+                        # batches k .. k + P - 1 = frame sets 0 .. P - 1 (contiguous in xb_all): one wavefront pass.  A
+                        # short last group is coded in a full pass as well (the missing partners' codes are dropped):
+                        # the encoder graph keeps one frame count, so no pass re-captures it
+                        rr_ = compress_side(ph, xb_all[:P_ * n])
                         rs_ = [split_record(rr_, e) for e in range(g)]
                         del rr_
                     for e, r_ in enumerate(rs_):
@@ -704,8 +712,8 @@ def main():
 
     # warmup: every decoder handle builds its row graphs, then `warmup` batches through the pipeline
     scratch = dict(encode=0.0, entropy=0.0, decode=0.0)
-    if args.team and args.enc_pass == 2:
-        compress_side(scratch, xb_all[:2 * n])       # the two-batch encoder graph (captured once)
+    if args.team and args.enc_pass > 1:
+        compress_side(scratch, xb_all[:args.enc_pass * n])       # the multi-batch encoder graph (captured once)
     r0 = compress_side(scratch, frames_of(0))
     st0 = entropy_side(r0, "reference", scratch)
     if not args.team:
@@ -729,6 +737,10 @@ def main():
                                                   team=args.team)
 
     side = {}
+    if args.side_steps > 0 and args.team and args.enc_pass > 1:
+        # the same schedule with every 32-frame batch encoded as its own wavefront pass (the round-5 headline's encoder)
+        d_, p_, _, _ = pipeline(args.steps, depth, label="one batch per encode pass", team=args.team, enc_pass=1)
+        side["one_batch_per_encode_pass"] = summary(d_, p_, args.steps, frames_per_encode_pass=n)
     if args.side_steps > 0 and args.team == 16 and args.team_batches == 1:
         # the round-4 geometry beside it: 8 teams per launch, one per XCD (each a whole XCD's CUs), same batches
         d_, p_, _, _ = pipeline(args.steps, depth, label="8 teams per launch", team=8)
@@ -801,6 +813,8 @@ def main():
     if args.team and team_acc["windows"] and len(team_acc["windows"]) > 1:
         first_teams = team_acc["windows"][0][3]          # teams of the first launch (the one beside the encoder)
     fts_used = args.first_team_size if args.first_team_size >= 0 else (12 if first_teams <= 8 else 0)
+    enc_desc = (f"{args.enc_pass} batches encoded in one {args.enc_pass * n}-frame wavefront pass" if args.team and
+                args.enc_pass > 1 else f"each batch encoded as its own {n}-frame wavefront pass")
     out = {
         "metric": METRIC if (args.config, H, W) == ("B8_lowrate", 768, 768) else
         f"Mpixels/s encode+decode, {args.config} N{N}M{M}, {W}×{H}", "value": round(value, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
@@ -810,11 +824,11 @@ def main():
                 "(no checkpoints / Kodak offline)",
         "config": {"workload": f"{args.config} N{N}M{M}, batches of {n} synthetic {H}x{W} frames per GPU, encode+decode "
                                f"in the reference bitstream format (one raster rANS stream per image); "
-                               + ((f"each batch encoded as its own {n}-frame wavefront pass and decoded as its own "
+                               + ((f"{enc_desc}, each batch entropy coded and decoded as its own "
                                    f"{n}-frame raster pass by one team of workgroups; up to {args.team} passes in one "
                                    "persistent launch (one team per XCD up to 8, two per XCD beyond)"
                                    if tb_cfg == 1 else
-                                   f"each batch encoded as its own {n}-frame wavefront pass; decode: {tb_cfg} batches per "
+                                   f"{enc_desc}; decode: {tb_cfg} batches per "
                                    f"team of workgroups ({n * tb_cfg} images per team side by side), up to {args.team} "
                                    "teams per launch")
                                   + (f"; the first launch (beside the encoder's next batches: {first_teams} teams) on "

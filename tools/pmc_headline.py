@@ -8,6 +8,7 @@ tools/team_exp.py (8 teams per k_dec_team launch); per team raster step = per di
 32-frame batch step (what bench.py scales by the batches a launch decodes) = per dispatch / (teams x images / 32 x Hb x Wb).
 """
 import json
+import os
 import sys
 
 
@@ -23,7 +24,7 @@ def main():
         if k in enc:
             res[k] = dict(dispatches=enc[k]["dispatches"], hbm_bytes_per_dispatch=enc[k]["hbm_bytes_per_dispatch"],
                           source="tools/enc_exp.py under FETCH_SIZE / WRITE_SIZE passes: the encoder graph of one "
-                                 "32-frame 768x768 B8_lowrate batch")
+                                 f"{os.environ.get('BATCH', '32')}-frame 768x768 B8_lowrate wavefront pass")
     fams = [enc.get(k, z) for k in ("k_gemm_t", "k_gemm", "k_gemm_s")]
     n = sum(f["dispatches"] for f in fams)
     res["encoder_graph"] = dict(dispatches=n, hbm_bytes_per_dispatch=sum(f["hbm_bytes_per_dispatch"] * f["dispatches"]
