@@ -33,7 +33,7 @@ def main():
             if k in enc and "hbm_bytes_per_dispatch" in enc[k]:
                 e[k] = dict(dispatches=enc[k]["dispatches"], hbm_bytes_per_dispatch=enc[k]["hbm_bytes_per_dispatch"],
                             source=f"tools/enc_exp.py under FETCH_SIZE / WRITE_SIZE passes: the {tag} encoder graph of "
-                                   f"one batch of {n} frames")
+                                   f"one wavefront pass of 4 batches of {n} frames (bench --enc-pass 4)")
         res[tag] = e
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1))
