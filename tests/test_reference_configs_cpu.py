@@ -139,11 +139,13 @@ def test_bench_roofline_dominance_is_wall_occupancy():
 
 def test_bench_team_schedule_defaults():
     """The headline's team schedule (bench.py defaults): 16 teams per launch, ONE 32-frame batch per team (each decode
-    pass decodes exactly one batch of the config), the first launch beside the encoder on 12 of every XCD's CUs; two
-    batches per team only for batches of at most 16 frames (configs 3 and 5)."""
+    pass decodes exactly one batch of the config), the first launch's footprint chosen by its team count (-1: 12
+    workgroups per XCD slot up to 8 teams, every CU beyond), four batches per encoder wavefront pass, the encoder's
+    copies on a stream of their own; two batches per team only for batches of at most 16 frames (configs 3 and 5)."""
     import bench
     a = bench.parse_args([])
-    assert (a.team, a.team_batches, a.first_team_size, a.batch) == (16, 1, 12, 32)
+    assert (a.team, a.team_batches, a.first_team_size, a.batch) == (16, 1, -1, 32)
+    assert (a.enc_pass, a.d2h_stream, a.steps) == (4, 1, 32)
     assert bench.parse_args(["--batch", "8"]).team_batches == 2
     assert bench.parse_args(["--batch", "24"]).team_batches == 1
     assert bench.parse_args(["--team-batches", "2"]).team_batches == 2
