@@ -381,6 +381,10 @@ def main():
         return v
 
     enc_acc = dict(on=False, ms=0.0, passes=0)     # HIP-event time of the encoder graphs in the timed region
+    # multi-batch encoder passes: the graph as ONE chain of launches (LBC_OPT_ENC_FORK 0; the library's own rule for
+    # passes this large), so the graphs' HIP-event wall time over their launches is the launches' average duration
+    enc_acc["chain"] = bool(args.team and args.enc_pass > 1)
+    enc_model.set_encoder_fork(0 if enc_acc["chain"] else -1)
 
     def compress_side(ph, xb, model=None, stream=None):
         """GPU compress on the encoder stream; symbols/indexes DMA'd into page-locked host buffers there (for the host
@@ -738,11 +742,19 @@ def main():
 
     side = {}
     if args.side_steps > 0 and args.team and args.enc_pass > 1:
-        # the same schedule with every 32-frame batch encoded as its own wavefront pass (the round-5 headline's encoder)
+        # the same schedule with every 32-frame batch encoded as its own wavefront pass (the round-5 headline's encoder,
+        # its graph forked as the library's default rule does for passes this small; captured before the leg)
+        enc_model.set_encoder_fork(-1)
+        entropy_side(compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), frames_of(0)), "reference",
+                     dict(encode=0.0, entropy=0.0, decode=0.0))
         d_, p_, _, _ = pipeline(args.steps, depth, label="one batch per encode pass", team=args.team, enc_pass=1)
         side["one_batch_per_encode_pass"] = summary(d_, p_, args.steps, frames_per_encode_pass=n)
+        enc_model.set_encoder_fork(0)
     if args.side_steps > 0 and args.team == 16 and args.team_batches == 1:
-        # the round-4 geometry beside it: 8 teams per launch, one per XCD (each a whole XCD's CUs), same batches
+        # the round-4 geometry beside it: 8 teams per launch, one per XCD (each a whole XCD's CUs), same batches (the
+        # headline's encoder graph captured again before the leg: a handle keeps one)
+        if args.enc_pass > 1:
+            compress_side(dict(encode=0.0, entropy=0.0, decode=0.0), xb_all[:args.enc_pass * n])
         d_, p_, _, _ = pipeline(args.steps, depth, label="8 teams per launch", team=8)
         side["eight_teams_per_launch"] = summary(d_, p_, args.steps, frames_in_flight_per_decode_pass=n,
                                                  decode_passes_in_flight=8)
@@ -916,7 +928,22 @@ def roofline(kstats, dt, team=None, enc=None, steps=0, cfg_key=None):
                        frac=round(tf / (enc["ms"] / 1e3) / (PEAK_FP32_TFLOPS * 1e12), 5),
                        note=f"every launch of the encoder graphs ({', '.join(k_ for k_ in efam if k_ in kstats)}): "
                             "algorithmic FLOPs / the graphs' wall time")
-            if sg.get("launches"):
+            if sg.get("launches") and enc.get("chain") and n_all == sg["total_launches"]:
+                # one chain of launches (no fork): HIP events around the graphs / the launches = a launch's average
+                # duration incl. the dependent-launch gap (an upper bound on the kernel time); the in-kernel stamps
+                # (earliest workgroup start -> latest end over the XCDs' clocks) are reported beside it
+                per = sg["total_ms"] / sg["launches"]
+                n_k = int(sg["total_launches"])
+                kernels[egm] = dict(launches_sampled=int(sg["launches"]), launches_total=n_k,
+                                    avg_span_us=round(wall * 1e3, 3), avg_launch_us=round(wall * 1e3, 3),
+                                    stamped_span_us=round(per * 1e3, 3), wall_us_per_launch=round(wall * 1e3, 3),
+                                    wall_occupancy_s=round(enc["ms"] / 1e3, 4),
+                                    summed_launch_s=round(enc["ms"] / 1e3, 4), aggregate=agg,
+                                    timing=f"HIP events around the encoder graphs (one chain of {n_k} launches: "
+                                           f"{enc['ms'] / 1e3:.3f} s over {enc['passes']} graphs) / their launches; "
+                                           f"in-kernel stamps of every sampled launch: stamped_span_us")
+                fam[egm] = (tf / n_all, tb / n_all)
+            elif sg.get("launches"):
                 per = sg["total_ms"] / sg["launches"]
                 n_k = int(sg["total_launches"])
                 kernels[egm] = dict(launches_sampled=int(sg["launches"]), launches_total=n_k,

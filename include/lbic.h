@@ -96,6 +96,12 @@ int lbc_encode(lbc_model *m, const float *x_dev, int n_img, int Hb, int Wb, floa
  * (default): CUs/8, every CU of an XCD.  Fewer: small teams (every workgroup then computes more output tiles and
  * decodes several rANS streams per step).  Results unchanged. */
 #define LBC_OPT_TEAM_SIZE 3
+/* LBC_OPT_ENC_FORK (-1, 0, 1): the encoder graph's wavefront steps as two branches (the context net beside the
+ * transform's first six GEMMs, joined before the quantising GEMM) or as one chain.  -1 (default): forked when the
+ * pass's largest wavefront step has at most 2,048 rows (a 32-frame 768^2 pass: 1,536), one chain for larger passes,
+ * whose launches fill the chip for several rounds each.  The environment's LBIC_ENC_FORK=0/1, when set, overrides it
+ * (experiments).  Results unchanged. */
+#define LBC_OPT_ENC_FORK 4
 int lbc_set_option(lbc_model *m, int option, long long value);
 
 /* lbc_encode with flags.  LBC_ENC_FRAME_PAD: the context net's layer-0 map is zero outside the frame

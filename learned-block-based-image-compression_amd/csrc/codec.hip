@@ -49,11 +49,17 @@ static int hip_rc(hipError_t e) {   // for code that must not return early (insi
 // Encoder graph fork: each wavefront step's context net (4 GEMMs) and the transform's first six GEMMs are independent
 // (only the quantising GEMM reads the means / scales), so they are captured as two branches joined before it.
 // Encoder alone 98.7 -> 95.0 ms per 32-frame batch, bit-identical; beside the team decoder within noise (+0.3..0.9 %;
-// profiles/r02_exp/encoder_fork_team.txt).  LBIC_ENC_FORK=0: one chain (with four busy streams, the workers schedule,
-// the branch's extra hardware queue cost 5 %: profiles/r02_exp/encoder_fork.txt).
-static bool enc_fork_on() {
+// profiles/r02_exp/encoder_fork_team.txt).  Only for passes whose largest wavefront step has at most ENC_FORK_MAX_ROWS
+// rows: a 128-frame pass's launches fill the chip for several rounds each, and two branches then only compete (bench,
+// four batches per pass: 136.0 / 133.3 Mpix/s with one chain vs 132.9 / 131.5 forked, profiles/r06/exp/fs_*).
+// LBIC_ENC_FORK=0 / 1 forces it (with four busy streams, the workers schedule, the branch's extra hardware queue cost
+// 5 %: profiles/r02_exp/encoder_fork.txt).
+// (LBC_OPT_ENC_FORK: -1 this rule, 0 / 1 forced)
+constexpr int ENC_FORK_MAX_ROWS = 2048;
+static bool enc_fork_on(int mmax, int opt) {
     const char* e = getenv("LBIC_ENC_FORK");
-    return !e || atoi(e) != 0;
+    if (e) return atoi(e) != 0;
+    return opt >= 0 ? opt != 0 : mmax <= ENC_FORK_MAX_ROWS;
 }
 
 struct DevBuf {
@@ -189,6 +195,7 @@ struct lbc_model {
     DevBuf l0, cells_enc;
     std::vector<int> cell_off, cell_cnt;
     int enc_lds_floor = 0;      // LBC_OPT_ENC_LDS_FLOOR
+    int enc_fork = -1;          // LBC_OPT_ENC_FORK
     int team_wpc = 1;           // LBC_OPT_TEAM_WG_PER_CU
     int team_size = 0;          // LBC_OPT_TEAM_SIZE (0: CUs / 8)
     Work lane[kLanes];
@@ -889,6 +896,7 @@ int lbc_create_sibling(const lbc_model* src, lbc_model** out) {
     m->NP = src->NP; m->C1P = src->C1P; m->C2P = src->C2P; m->C3P = src->C3P;
     m->l0_on = src->l0_on;
     m->enc_lds_floor = src->enc_lds_floor;
+    m->enc_fork = src->enc_fork;
     m->net = src->net;                    // shared, read-only
     m->finalized = true;
     if (src->tabs_set) {                  // host copies; this handle uploads its own device tables on first use
@@ -917,6 +925,10 @@ int lbc_set_option(lbc_model* m, int option, long long value) {
         case LBC_OPT_TEAM_SIZE:
             if (value < 0 || value > 32) return set_error(LBC_E_ARG, "team size must be 0 (CUs / 8) .. 32");
             m->team_size = (int)value;
+            return LBC_OK;
+        case LBC_OPT_ENC_FORK:
+            if (value < -1 || value > 1) return set_error(LBC_E_ARG, "encoder fork must be -1 (auto), 0 or 1");
+            m->enc_fork = (int)value;
             return LBC_OK;
     }
     return set_error(LBC_E_ARG, "unknown option");
@@ -1065,7 +1077,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
     const std::vector<long long> key = {n_img, Hb, Wb, (long long)m->x_in.p, (long long)m->zpad.p,
                                         (long long)m->sym_buf.p, (long long)m->lane[0].ctx0.p,
                                         (long long)m->table_dev.p, m->prof.sample_every, flags,
-                                        m->enc_lds_floor};
+                                        m->enc_lds_floor, m->enc_fork};
     if (!m->enc_exec || key != m->enc_key) {
         std::lock_guard<std::mutex> lk(g_capture_mu);
         if (m->enc_exec) { (void)hipGraphExecDestroy(m->enc_exec); m->enc_exec = nullptr; }
@@ -1073,7 +1085,7 @@ int lbc_encode_ex(lbc_model* m, const float* x_dev, int n_img, int Hb, int Wb, f
         int crc = prof_range_begin(&m->prof, 0, m->cap);
         drop_recs(m->prof, 0);
         const int4* blocks = m->blocks_enc.as<int4>();
-        const bool fork = enc_fork_on();   // (sampled: launch spans only, no launch-to-launch period)
+        const bool fork = enc_fork_on(m->Mmax, m->enc_fork);   // (sampled: launch spans only, no launch-to-launch period)
         g_prof = &m->prof;
         m->prof.nochain = fork;
         for (size_t t = 0; t < m->step_off.size(); ++t)

@@ -337,6 +337,11 @@ class BlockBasedImgCompLossyNetv9:
         room for a decoder on another stream).  Performance only; results are unchanged."""
         _lib.check(_lib.lib().lbc_set_option(self._h, 1, int(nbytes)))
 
+    def set_encoder_fork(self, mode: int):
+        """LBC_OPT_ENC_FORK: -1 (default) the encoder graph forks its wavefront steps (context net beside the
+        transform) only for passes of at most 2,048 rows per step; 0 one chain; 1 forked.  Results unchanged."""
+        _lib.check(_lib.lib().lbc_set_option(self._h, 4, int(mode)))
+
     def validate_recu_reco(self, x: torch.Tensor):
         """The recursive reconstruction of BlockBasedImgCompLossyAgent.validate_recu_reco_fast
         (agents/blkbsdimgcomp_agent.py:491-520): raster closed loop of forward() on causal crops, i.e. the

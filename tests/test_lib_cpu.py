@@ -107,3 +107,25 @@ def test_errors_are_loud():
     out = np.zeros(3, np.uint32)
     with pytest.raises(RuntimeError):
         _lib.check(L.lbc_pmf_to_quantized_cdf(_lib.ptr(bad), 2, 16, _lib.ptr(out)))
+
+
+def test_set_option_ranges():
+    """lbc_set_option (host-only, no GPU): every option's range is checked, LBC_OPT_ENC_FORK takes -1 / 0 / 1 (the
+    encoder graph forked by the pass's row count, one chain, forked), an unknown option is an error."""
+    L = _lib.lib()
+    cfg = _lib.LbcConfig()
+    cfg.block_size, cfg.n, cfg.m, cfg.device = 4, 64, 16, 0
+    for i, k in enumerate((3, 1, 1, 1)):
+        cfg.ks[i] = k
+    h = ctypes.c_void_p()
+    _lib.check(L.lbc_create(ctypes.byref(cfg), ctypes.byref(h)))
+    try:
+        for opt, good, bad in ((1, (0, 65536), (-1, 160 * 1024 + 1)), (2, (1, 2), (0, 3)), (3, (0, 32), (-1, 33)),
+                               (4, (-1, 0, 1), (-2, 2))):
+            for v in good:
+                assert L.lbc_set_option(h, opt, v) == 0, (opt, v)
+            for v in bad:
+                assert L.lbc_set_option(h, opt, v) != 0, (opt, v)
+        assert L.lbc_set_option(h, 99, 0) != 0
+    finally:
+        L.lbc_destroy(h)

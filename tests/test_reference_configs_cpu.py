@@ -137,6 +137,28 @@ def test_bench_roofline_dominance_is_wall_occupancy():
     assert roof["kernel"] == "k_gemm_t" and roof["bound"] == "mfma"
 
 
+def test_bench_roofline_single_chain_encoder():
+    """Multi-batch encoder passes run the encoder graph as ONE chain of launches (LBC_OPT_ENC_FORK 0): the k_gemm launch
+    duration of the bench line is then the graphs' HIP-event wall time over their launches (an upper bound incl. the
+    dependent-launch gap), the in-kernel stamps reported beside it; the per-launch work is the family's total over its
+    launches."""
+    import bench
+    dt, steps = 4.6, 32
+    kstats = {"k_gemm": dict(launches=2600, total_launches=41184, total_ms=2600 * 0.0866, flops=4.3e9, bytes=3.6e7,
+                             total_flops=41184 * 4.12e9, total_bytes=41184 * 3.5e7)}
+    enc = dict(ms=41184 * 0.0781, passes=8, chain=True)
+    team = dict(launches=2, ms=2800.0, bytes=2 * 1.9e12, flops=2 * 2.8e13, steps=32 * 9216, plain=[1, 1],
+                timeouts=0, hw=9216, windows=[[1.1, 2.8, 16, 16], [3.3, 4.5, 16, 16]], enc_done=3.3)
+    roof, kernels = bench.roofline(kstats, dt, team, enc, steps)
+    k = kernels["k_gemm"]
+    assert roof["kernel"] == "k_gemm" and roof["bound"] == "mfma"
+    assert abs(k["avg_launch_us"] - 78.1) < 0.01 and abs(k["stamped_span_us"] - 86.6) < 0.01
+    assert abs(roof["achieved"] - 4.12e9 / 78.1e-6 / 1e12) < 1e-3
+    enc["chain"] = False          # a forked graph: the stamps give the launch's own duration
+    _, kernels = bench.roofline(kstats, dt, team, enc, steps)
+    assert abs(kernels["k_gemm"]["avg_launch_us"] - 86.6) < 0.01
+
+
 def test_bench_team_schedule_defaults():
     """The headline's team schedule (bench.py defaults): 16 teams per launch, ONE 32-frame batch per team (each decode
     pass decodes exactly one batch of the config), the first launch's footprint chosen by its team count (-1: 12
