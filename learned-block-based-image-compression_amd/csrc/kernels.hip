@@ -370,6 +370,12 @@ int launch_gemm(const GemmArgs& g0, hipStream_t s, int* cfg_id) {
     // register caps that spill (64 / 80 VGPRs) 116.7 / 115.8.  Beside the team decoder (bench.py --steps 20):
     // 84.9 Mpix/s against 79.7 for the earlier default.  (Other tiles, XCD-aware and 2-D XCD tile orders: measured
     // in rounds 2-3 and removed)
+    static const int tile = [] {       // experiment hook: LBIC_ENC_TILE=1 -> 32 x 32 tiles (round 6, 128-frame passes)
+        const char* e = getenv("LBIC_ENC_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    if (tile == 1) return launch_cfg<32, 32, 8, 1>(g, s);
+    if (tile == 2) return launch_cfg<16, 64, 8, 1>(g, s);
     return launch_cfg<16, 32, 8, 1>(g, s);
 }
 
