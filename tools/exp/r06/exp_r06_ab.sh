@@ -1,5 +1,5 @@
 #!/bin/bash
-# same-box A/B of team-kernel variants: tools/exp_r06_ab.sh OUT REPS V1 V2 ... (cur = liblbic.so); team_exp at 16 teams
+# same-box A/B of team-kernel variants: tools/exp/r06/exp_r06_ab.sh OUT REPS V1 V2 ... (cur = liblbic.so); team_exp at 16 teams
 set -o pipefail
 out=$1; reps=$2; shift 2
 mkdir -p gpurun_out/r06

@@ -2,7 +2,7 @@
 # r06 call 13: team prologue quotients (cur vs thead), encoder single-segment k_gemm (cur vs khead), parity tests
 set -eo pipefail
 mkdir -p gpurun_out/r06
-bash tools/exp_r06_ab.sh gpurun_out/r06/c13_ab.log 2 thead cur
+bash tools/exp/r06/exp_r06_ab.sh gpurun_out/r06/c13_ab.log 2 thead cur
 for rep in 1 2; do
   for v in khead cur; do
     if [ $v = cur ]; then unset LBIC_LIB_VARIANT; else export LBIC_LIB_VARIANT=$v; fi
