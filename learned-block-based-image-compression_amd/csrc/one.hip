@@ -576,6 +576,15 @@ __device__ __forceinline__ bool one_gemm_any(const OneArgs& a, const OneOp& op, 
     const int nkb = op.K >> 4;
     const bool l0 = KL0 && (op.l0out || op.l0seg);
     int key = (nkb / KSPLIT) * 2 + (nkb % KSPLIT == 0 ? 1 : 0);
+    if constexpr (KL0) {     // the layer-0-cache kernel (B4_highrate: K = 384 / 512 / 640): exact slices of 3-5
+                             // k-blocks, no discarded fragment (only this kernel carries the instances)
+        if (!l0) switch (key) {
+            case 7: return one_gemm<3, false>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
+            case 9: return one_gemm<4, false>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
+            case 11: return one_gemm<5, false>(a, op, o, my, v, h, tag, wl, red, scr, sflag, c, lst, ltab);
+            default: break;
+        }
+    }
 #ifndef LBIC_ONE_EXACT_ALL
     if ((key & 1) && key != 13 && key != 19) key &= ~1;     // exact slices without an instance: the L + 1 form
 #endif
